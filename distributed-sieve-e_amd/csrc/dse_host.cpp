@@ -1,0 +1,575 @@
+// dse_host.cpp -- C-ABI host layer of libdse.so (include/dse.h).
+//
+// Replaces the reference's orchestration of the hot path:
+//   spread-work (sieve.clj:15-34)            -> dse_spread_work (exact int64)
+//   gen-table + sieve-e (sieve.clj:9-172)    -> dse_sieve_chunk / dse_sieve_all
+//   per-prime [mi ps p] relay through the
+//     lead (sieve.clj:139, core.clj:118-134) -> one RCCL broadcast of base primes
+//   (no result gather in the reference)      -> RCCL all-reduce of counts
+//   finish (sieve.clj:82-108)                -> dse_write_primes_file
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/dse.h"
+#include "dse_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int32_t fail(int32_t code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                     \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess)                                                                 \
+      return fail(DSE_EHIP, std::string(#expr " failed: ") + hipGetErrorString(e_));      \
+  } while (0)
+
+#define NCCL_TRY(expr)                                                                    \
+  do {                                                                                    \
+    ncclResult_t r_ = (expr);                                                             \
+    if (r_ != ncclSuccess)                                                                \
+      return fail(DSE_ENCCL, std::string(#expr " failed: ") + ncclGetErrorString(r_));    \
+  } while (0)
+
+uint64_t isqrt_u64(uint64_t x) {
+  uint64_t r = (uint64_t)std::sqrt((long double)x);
+  while (r > 0 && r * r > x) --r;
+  while ((r + 1) * (r + 1) <= x) ++r;
+  return r;
+}
+
+// Upper bound on the number of odd primes <= x (Rosser-Schoenfeld
+// pi(x) < 1.25506 x / ln x for x > 1), padded.
+uint32_t prime_cap(uint64_t x) {
+  if (x < 100) return 64;
+  double b = 1.25506 * (double)x / std::log((double)x);
+  return (uint32_t)b + 64;
+}
+
+struct ChunkMask {
+  int32_t my_num = 0;
+  uint64_t* dev_ptr = nullptr;
+  uint64_t words = 0;
+};
+
+struct DevState {
+  int device = 0;
+  int num_cus = 0;
+  hipStream_t stream = nullptr;
+  void* table = nullptr;
+  uint64_t table_bytes = 0;
+  unsigned long long* counts = nullptr;  // device scratch
+  uint64_t counts_len = 0;
+  uint64_t* scratch_mask = nullptr;      // for dse_sieve_chunk
+  uint64_t scratch_words = 0;
+  std::vector<ChunkMask> resident;       // masks kept by dse_sieve_all
+};
+
+}  // namespace
+
+struct dse_ctx {
+  std::vector<DevState> devs;
+  std::vector<ncclComm_t> comms;
+  int64_t last_n = -1;
+  int32_t last_P = 0;
+};
+
+namespace {
+
+int32_t ensure_table(DevState& d, uint64_t limit) {
+  const uint64_t need = dse_base_table_bytes(limit);
+  if (d.table_bytes < need) {
+    if (d.table) HIP_TRY(hipFree(d.table));
+    d.table = nullptr;
+    d.table_bytes = 0;
+    HIP_TRY(hipMalloc(&d.table, need));
+    d.table_bytes = need;
+  }
+  return DSE_OK;
+}
+
+int32_t ensure_counts(DevState& d, uint64_t n) {
+  if (d.counts_len < n) {
+    if (d.counts) HIP_TRY(hipFree(d.counts));
+    d.counts = nullptr;
+    d.counts_len = 0;
+    HIP_TRY(hipMalloc(&d.counts, n * sizeof(unsigned long long)));
+    d.counts_len = n;
+  }
+  return DSE_OK;
+}
+
+int32_t build_table(DevState& d, uint64_t limit) {
+  if (limit > dse::kBaseLimitMax)
+    return fail(DSE_ERANGE, "base-prime limit " + std::to_string(limit) + " above the supported " +
+                                std::to_string(dse::kBaseLimitMax));
+  int32_t rc = ensure_table(d, limit);
+  if (rc) return rc;
+  HIP_TRY(dse::launch_base_primes(limit, d.table, prime_cap(limit), d.stream));
+  return DSE_OK;
+}
+
+int32_t free_resident(DevState& d) {
+  for (auto& c : d.resident)
+    if (c.dev_ptr) HIP_TRY(hipFree(c.dev_ptr));
+  d.resident.clear();
+  return DSE_OK;
+}
+
+int32_t chunk_geometry(int64_t n, int32_t P, int64_t* cs) {
+  if (P < 1) return fail(DSE_EINVAL, "num-comps must be >= 1");
+  if (n < 0) return fail(DSE_EINVAL, "n must be >= 0");
+  int64_t nums = n >= 1 ? (n - 1) / 2 : 0;
+  *cs = nums / P;
+  return DSE_OK;
+}
+
+int32_t init_dev(DevState& d, int device) {
+  d.device = device;
+  HIP_TRY(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  d.num_cus = prop.multiProcessorCount;
+  HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  return DSE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* dse_version(void) { return "dse 0.1 gfx950"; }
+
+const char* dse_last_error(void) { return g_err.c_str(); }
+
+int32_t dse_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+dse_ctx* dse_init(int32_t num_gpus) {
+  int avail = 0;
+  if (hipGetDeviceCount(&avail) != hipSuccess || avail < 1) {
+    fail(DSE_EHIP, "no HIP device visible");
+    return nullptr;
+  }
+  if (num_gpus <= 0) num_gpus = avail;
+  if (num_gpus > avail) {
+    fail(DSE_EINVAL, "asked for " + std::to_string(num_gpus) + " GPUs, " + std::to_string(avail) + " visible");
+    return nullptr;
+  }
+  dse_ctx* ctx = new dse_ctx();
+  ctx->devs.resize(num_gpus);
+  for (int i = 0; i < num_gpus; ++i)
+    if (init_dev(ctx->devs[i], i) != DSE_OK) {
+      dse_destroy(ctx);
+      return nullptr;
+    }
+  if (num_gpus > 1) {
+    ctx->comms.resize(num_gpus);
+    std::vector<int> ids(num_gpus);
+    for (int i = 0; i < num_gpus; ++i) ids[i] = i;
+    ncclResult_t r = ncclCommInitAll(ctx->comms.data(), num_gpus, ids.data());
+    if (r != ncclSuccess) {
+      fail(DSE_ENCCL, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+      ctx->comms.clear();
+      dse_destroy(ctx);
+      return nullptr;
+    }
+  }
+  return ctx;
+}
+
+dse_ctx* dse_init_device(int32_t device) {
+  int avail = 0;
+  if (hipGetDeviceCount(&avail) != hipSuccess || device < 0 || device >= avail) {
+    fail(DSE_EINVAL, "device " + std::to_string(device) + " not visible");
+    return nullptr;
+  }
+  dse_ctx* ctx = new dse_ctx();
+  ctx->devs.resize(1);
+  if (init_dev(ctx->devs[0], device) != DSE_OK) {
+    dse_destroy(ctx);
+    return nullptr;
+  }
+  return ctx;
+}
+
+void dse_destroy(dse_ctx* ctx) {
+  if (!ctx) return;
+  for (auto& c : ctx->comms) ncclCommDestroy(c);
+  for (auto& d : ctx->devs) {
+    (void)hipSetDevice(d.device);
+    free_resident(d);
+    if (d.table) (void)hipFree(d.table);
+    if (d.counts) (void)hipFree(d.counts);
+    if (d.scratch_mask) (void)hipFree(d.scratch_mask);
+    if (d.stream) (void)hipStreamDestroy(d.stream);
+  }
+  delete ctx;
+}
+
+int32_t dse_ctx_num_devices(const dse_ctx* ctx) { return ctx ? (int32_t)ctx->devs.size() : 0; }
+
+int32_t dse_spread_work(int64_t n, int32_t P, int64_t* lo_hi, int64_t* cs) {
+  int64_t c;
+  int32_t rc = chunk_geometry(n, P, &c);
+  if (rc) return rc;
+  if (cs) *cs = c;
+  if (lo_hi)
+    for (int32_t k = 1; k <= P; ++k) {
+      lo_hi[2 * (k - 1)] = 3 + 2 * (int64_t)(k - 1) * c;
+      lo_hi[2 * (k - 1) + 1] = 3 + 2 * (int64_t)k * c;
+    }
+  return DSE_OK;
+}
+
+int32_t dse_tail_range(int64_t n, int32_t P, uint64_t* g_start, uint64_t* nbits) {
+  int64_t cs;
+  int32_t rc = chunk_geometry(n, P, &cs);
+  if (rc) return rc;
+  int64_t nums = n >= 1 ? (n - 1) / 2 : 0;
+  if (g_start) *g_start = (uint64_t)(P * cs);
+  if (nbits) *nbits = (uint64_t)(nums - P * cs);
+  return DSE_OK;
+}
+
+uint64_t dse_base_table_bytes(uint64_t limit) { return dse::table_bytes_for_cap(prime_cap(limit)); }
+
+uint64_t dse_base_limit_max(void) { return dse::kBaseLimitMax; }
+
+uint64_t dse_base_limit_for_range(uint64_t g_start, uint64_t nbits) {
+  if (nbits == 0) return 0;
+  const uint64_t vmax = 3 + 2 * (g_start + nbits - 1);
+  return isqrt_u64(vmax);
+}
+
+int32_t dse_base_primes_dev_async(dse_ctx* ctx, uint64_t limit, void* table_dev, uint64_t table_bytes,
+                                  void* stream) {
+  if (!ctx || !table_dev) return fail(DSE_EINVAL, "null ctx or table");
+  if (table_bytes < dse_base_table_bytes(limit)) return fail(DSE_EINVAL, "table buffer too small");
+  if (limit > dse::kBaseLimitMax) return fail(DSE_ERANGE, "base-prime limit above the supported maximum");
+  HIP_TRY(hipSetDevice(ctx->devs[0].device));
+  HIP_TRY(dse::launch_base_primes(limit, table_dev, prime_cap(limit), (hipStream_t)stream));
+  return DSE_OK;
+}
+
+int32_t dse_sieve_range_dev_async(dse_ctx* ctx, const void* table_dev, uint64_t g_start, uint64_t nbits,
+                                  uint64_t* mask_dev, uint64_t* count_dev, void* stream) {
+  if (!ctx || !table_dev || !count_dev) return fail(DSE_EINVAL, "null ctx, table or count");
+  if (g_start > (1ull << 62) || nbits > (1ull << 62) - g_start)
+    return fail(DSE_ERANGE, "odd-index range beyond 2^62");
+  HIP_TRY(hipSetDevice(ctx->devs[0].device));
+  HIP_TRY(dse::launch_sieve_range(table_dev, g_start, nbits, reinterpret_cast<uint32_t*>(mask_dev),
+                                  reinterpret_cast<unsigned long long*>(count_dev), ctx->devs[0].num_cus,
+                                  (hipStream_t)stream));
+  return DSE_OK;
+}
+
+namespace {
+int32_t sieve_range_host(dse_ctx* ctx, DevState& d, uint64_t g0, uint64_t nbits, uint64_t* mask_or_null,
+                         uint64_t* count) {
+  int32_t rc;
+  HIP_TRY(hipSetDevice(d.device));
+  const uint64_t words = (nbits + 63) / 64;
+  if ((rc = build_table(d, dse_base_limit_for_range(g0, nbits)))) return rc;
+  if ((rc = ensure_counts(d, 1))) return rc;
+  if (mask_or_null && d.scratch_words < words) {
+    if (d.scratch_mask) HIP_TRY(hipFree(d.scratch_mask));
+    d.scratch_mask = nullptr;
+    d.scratch_words = 0;
+    HIP_TRY(hipMalloc(&d.scratch_mask, words * 8));
+    d.scratch_words = words;
+  }
+  HIP_TRY(hipMemsetAsync(d.counts, 0, sizeof(unsigned long long), d.stream));
+  HIP_TRY(dse::launch_sieve_range(d.table, g0, nbits,
+                                  mask_or_null ? reinterpret_cast<uint32_t*>(d.scratch_mask) : nullptr,
+                                  d.counts, d.num_cus, d.stream));
+  unsigned long long c = 0;
+  HIP_TRY(hipMemcpyAsync(&c, d.counts, sizeof(c), hipMemcpyDeviceToHost, d.stream));
+  if (mask_or_null && words)
+    HIP_TRY(hipMemcpyAsync(mask_or_null, d.scratch_mask, words * 8, hipMemcpyDeviceToHost, d.stream));
+  HIP_TRY(hipStreamSynchronize(d.stream));
+  if (count) *count = c;
+  (void)ctx;
+  return DSE_OK;
+}
+}  // namespace
+
+int32_t dse_sieve_odd_range(dse_ctx* ctx, uint64_t g_start, uint64_t nbits, uint64_t* mask_or_null,
+                            uint64_t* count) {
+  if (!ctx) return fail(DSE_EINVAL, "null ctx");
+  if (g_start > (1ull << 62) || nbits > (1ull << 62) - g_start)
+    return fail(DSE_ERANGE, "odd-index range beyond 2^62");
+  return sieve_range_host(ctx, ctx->devs[0], g_start, nbits, mask_or_null, count);
+}
+
+int32_t dse_sieve_chunk(dse_ctx* ctx, int64_t n, int32_t P, int32_t my_num, uint64_t* mask_or_null,
+                        uint64_t* count) {
+  if (!ctx) return fail(DSE_EINVAL, "null ctx");
+  int64_t cs;
+  int32_t rc = chunk_geometry(n, P, &cs);
+  if (rc) return rc;
+  if (my_num < 1 || my_num > P) return fail(DSE_EINVAL, "my_num outside 1..P");
+  if (cs < 1) return fail(DSE_EINVAL, "empty chunk (find-first-prime would throw)");
+  DevState& d = ctx->devs[(my_num - 1) % ctx->devs.size()];
+  return sieve_range_host(ctx, d, (uint64_t)(my_num - 1) * (uint64_t)cs, (uint64_t)cs, mask_or_null, count);
+}
+
+int32_t dse_sieve_all(dse_ctx* ctx, int64_t n, int32_t P, uint64_t* per_chunk_counts, uint64_t* pi_ref,
+                      uint64_t* pi_full) {
+  if (!ctx) return fail(DSE_EINVAL, "null ctx");
+  int64_t cs;
+  int32_t rc = chunk_geometry(n, P, &cs);
+  if (rc) return rc;
+  if (cs < 1) return fail(DSE_EINVAL, "empty chunk (find-first-prime would throw)");
+  uint64_t tail_g, tail_n;
+  dse_tail_range(n, P, &tail_g, &tail_n);
+  const int nd = (int)ctx->devs.size();
+  const uint64_t words = ((uint64_t)cs + 63) / 64;
+  // every chunk and the tail are covered by the primes <= sqrt(largest odd <= n)
+  const uint64_t limit = dse_base_limit_for_range(0, (uint64_t)P * (uint64_t)cs + tail_n);
+  const uint64_t nc = (uint64_t)P + 1;  // per-chunk counts + tail
+
+  // resident masks: one device buffer per chunk, on its device
+  for (int i = 0; i < nd; ++i) {
+    DevState& d = ctx->devs[i];
+    HIP_TRY(hipSetDevice(d.device));
+    bool reuse = ctx->last_n >= 0 && ctx->last_P == P && !d.resident.empty() && d.resident[0].words == words;
+    if (!reuse) {
+      if ((rc = free_resident(d))) return rc;
+      for (int32_t k = i + 1; k <= P; k += nd) {
+        ChunkMask cm;
+        cm.my_num = k;
+        cm.words = words;
+        HIP_TRY(hipMalloc(&cm.dev_ptr, words * 8));
+        d.resident.push_back(cm);
+      }
+    } else {
+      for (auto& cm : d.resident) cm.my_num = cm.my_num;  // same layout as last call
+    }
+    if ((rc = ensure_table(d, limit))) return rc;
+    if ((rc = ensure_counts(d, nc))) return rc;
+    HIP_TRY(hipMemsetAsync(d.counts, 0, nc * sizeof(unsigned long long), d.stream));
+  }
+  ctx->last_n = n;
+  ctx->last_P = P;
+
+  // base primes once, on device 0; RCCL broadcast to the others
+  HIP_TRY(hipSetDevice(ctx->devs[0].device));
+  if ((rc = build_table(ctx->devs[0], limit))) return rc;
+  const uint64_t tbytes = dse_base_table_bytes(limit);
+  if (nd > 1) {
+    NCCL_TRY(ncclGroupStart());
+    for (int i = 0; i < nd; ++i) {
+      DevState& d = ctx->devs[i];
+      NCCL_TRY(ncclBroadcast(ctx->devs[0].table, d.table, tbytes, ncclUint8, 0, ctx->comms[i], d.stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+  }
+
+  // each device sieves its chunks; the last device also sieves the tail
+  for (int i = 0; i < nd; ++i) {
+    DevState& d = ctx->devs[i];
+    HIP_TRY(hipSetDevice(d.device));
+    for (auto& cm : d.resident) {
+      const uint64_t g0 = (uint64_t)(cm.my_num - 1) * (uint64_t)cs;
+      HIP_TRY(dse::launch_sieve_range(d.table, g0, (uint64_t)cs, reinterpret_cast<uint32_t*>(cm.dev_ptr),
+                                      d.counts + (cm.my_num - 1), d.num_cus, d.stream));
+    }
+    if (i == nd - 1 && tail_n)
+      HIP_TRY(dse::launch_sieve_range(d.table, tail_g, tail_n, nullptr, d.counts + P, d.num_cus, d.stream));
+  }
+
+  // counts: RCCL all-reduce (each slot is non-zero on exactly one device)
+  if (nd > 1) {
+    NCCL_TRY(ncclGroupStart());
+    for (int i = 0; i < nd; ++i) {
+      DevState& d = ctx->devs[i];
+      NCCL_TRY(ncclAllReduce(d.counts, d.counts, nc, ncclUint64, ncclSum, ctx->comms[i], d.stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+  }
+  std::vector<unsigned long long> h(nc);
+  HIP_TRY(hipSetDevice(ctx->devs[0].device));
+  HIP_TRY(hipMemcpyAsync(h.data(), ctx->devs[0].counts, nc * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                         ctx->devs[0].stream));
+  for (int i = 0; i < nd; ++i) {
+    HIP_TRY(hipSetDevice(ctx->devs[i].device));
+    HIP_TRY(hipStreamSynchronize(ctx->devs[i].stream));
+  }
+  uint64_t sum = 0;
+  for (int32_t k = 0; k < P; ++k) {
+    if (per_chunk_counts) per_chunk_counts[k] = h[k];
+    sum += h[k];
+  }
+  if (pi_ref) *pi_ref = 1 + sum;
+  if (pi_full) *pi_full = 1 + sum + h[P];
+  return DSE_OK;
+}
+
+int32_t dse_copy_chunk_mask(dse_ctx* ctx, int32_t my_num, uint64_t* mask) {
+  if (!ctx || !mask) return fail(DSE_EINVAL, "null ctx or mask");
+  for (auto& d : ctx->devs)
+    for (auto& cm : d.resident)
+      if (cm.my_num == my_num) {
+        HIP_TRY(hipSetDevice(d.device));
+        HIP_TRY(hipMemcpyAsync(mask, cm.dev_ptr, cm.words * 8, hipMemcpyDeviceToHost, d.stream));
+        HIP_TRY(hipStreamSynchronize(d.stream));
+        return DSE_OK;
+      }
+  return fail(DSE_EINVAL, "chunk " + std::to_string(my_num) + " is not resident");
+}
+
+int32_t dse_sieve_window(dse_ctx* ctx, uint64_t lo, uint64_t hi, uint64_t* count) {
+  if (!ctx || !count) return fail(DSE_EINVAL, "null ctx or count");
+  *count = 0;
+  uint64_t a = lo < 3 ? 3 : lo;
+  if (!(a & 1)) ++a;
+  if (hi < a) return DSE_OK;
+  const uint64_t b = (hi & 1) ? hi : hi - 1;
+  const uint64_t g0 = (a - 3) / 2, nb = (b - a) / 2 + 1;
+  const uint64_t limit = dse_base_limit_for_range(g0, nb);
+  if (limit > dse::kBaseLimitMax)
+    return fail(DSE_ERANGE, "window needs base primes up to " + std::to_string(limit) +
+                                "; the device base-prime kernel supports " + std::to_string(dse::kBaseLimitMax));
+  const int nd = (int)ctx->devs.size();
+  int32_t rc;
+  for (int i = 0; i < nd; ++i) {
+    DevState& d = ctx->devs[i];
+    HIP_TRY(hipSetDevice(d.device));
+    if ((rc = ensure_counts(d, 1))) return rc;
+    if ((rc = build_table(d, limit))) return rc;
+    HIP_TRY(hipMemsetAsync(d.counts, 0, sizeof(unsigned long long), d.stream));
+    const uint64_t part = (nb + nd - 1) / nd;
+    const uint64_t s = std::min<uint64_t>(nb, part * i), e = std::min<uint64_t>(nb, part * (i + 1));
+    if (e > s) HIP_TRY(dse::launch_sieve_range(d.table, g0 + s, e - s, nullptr, d.counts, d.num_cus, d.stream));
+  }
+  uint64_t total = 0;
+  for (int i = 0; i < nd; ++i) {
+    DevState& d = ctx->devs[i];
+    HIP_TRY(hipSetDevice(d.device));
+    unsigned long long c = 0;
+    HIP_TRY(hipMemcpyAsync(&c, d.counts, sizeof(c), hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    total += c;
+  }
+  *count = total;
+  return DSE_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// finish writer (sieve.clj:82-108)
+// ---------------------------------------------------------------------------
+namespace {
+
+inline int fmt_u64(uint64_t v, char* out) {
+  char t[24];
+  int n = 0;
+  do {
+    t[n++] = (char)('0' + v % 10);
+    v /= 10;
+  } while (v);
+  for (int i = 0; i < n; ++i) out[i] = t[n - 1 - i];
+  return n;
+}
+
+// java.lang.Double.toString of an integer-valued double 1 <= v < 2^53.
+inline int fmt_java_double(uint64_t v, char* out) {
+  if (v < 10000000ull) {
+    int n = fmt_u64(v, out);
+    out[n++] = '.';
+    out[n++] = '0';
+    return n;
+  }
+  char d[24];
+  int len = fmt_u64(v, d);
+  int sig = len;
+  while (sig > 1 && d[sig - 1] == '0') --sig;
+  int n = 0;
+  out[n++] = d[0];
+  out[n++] = '.';
+  if (sig == 1) out[n++] = '0';
+  for (int i = 1; i < sig; ++i) out[n++] = d[i];
+  out[n++] = 'E';
+  n += fmt_u64((uint64_t)(len - 1), out + n);
+  return n;
+}
+
+}  // namespace
+
+extern "C" int32_t dse_write_range_file(const char* path, int32_t my_num, uint64_t g_start, uint64_t nbits,
+                                        const uint64_t* mask) {
+  if (!path || !mask) return fail(DSE_EINVAL, "null path or mask");
+  if (my_num < 1) return fail(DSE_EINVAL, "my_num must be >= 1");
+  if (my_num == 1 && nbits < 4) return fail(DSE_EINVAL, "finish's 2/3/5/7 hack needs a chunk of >= 4 candidates");
+  const uint64_t cs = nbits;
+  FILE* f = std::fopen(path, "wb");
+  if (!f) return fail(DSE_EIO, std::string("cannot open ") + path);
+  std::vector<char> buf(1 << 20);
+  size_t used = 0;
+  int per_line = 0;
+  const uint64_t base = g_start;
+  auto emit = [&](uint64_t v) {
+    if (used + 64 > buf.size()) {
+      std::fwrite(buf.data(), 1, used, f);
+      used = 0;
+    }
+    if (per_line) {
+      buf[used++] = ',';
+      buf[used++] = ' ';
+    }
+    used += (size_t)(my_num == 1 ? fmt_java_double(v, buf.data() + used) : fmt_u64(v, buf.data() + used));
+    if (++per_line == 10) {
+      buf[used++] = '\n';
+      per_line = 0;
+    }
+  };
+  const uint64_t words = (cs + 63) / 64;
+  uint64_t j0 = 0;
+  if (my_num == 1) {  // positions 0..3 become 2.0 3.0 5.0 7.0 (sieve.clj:93-96)
+    emit(2);
+    emit(3);
+    emit(5);
+    emit(7);
+    j0 = 4;
+  }
+  for (uint64_t w = j0 / 64; w < words; ++w) {
+    uint64_t v = mask[w];
+    if (w == j0 / 64) v &= ~0ull << (j0 % 64);
+    if (w == words - 1 && (cs & 63)) v &= (1ull << (cs & 63)) - 1;
+    while (v) {
+      const int b = __builtin_ctzll(v);
+      v &= v - 1;
+      emit(3 + 2 * (base + w * 64 + (uint64_t)b));
+    }
+  }
+  if (per_line) buf[used++] = '\n';
+  std::fwrite(buf.data(), 1, used, f);
+  if (std::fclose(f) != 0) return fail(DSE_EIO, std::string("write failed: ") + path);
+  return DSE_OK;
+}
+
+extern "C" int32_t dse_write_primes_file(const char* path, int32_t my_num, int64_t n, int32_t P,
+                                         const uint64_t* mask) {
+  int64_t cs;
+  int32_t rc = chunk_geometry(n, P, &cs);
+  if (rc) return rc;
+  if (my_num < 1 || my_num > P) return fail(DSE_EINVAL, "my_num outside 1..P");
+  if (cs < 4) return fail(DSE_EINVAL, "finish's 2/3/5/7 hack needs a chunk of >= 4 candidates");
+  return dse_write_range_file(path, my_num, (uint64_t)(my_num - 1) * (uint64_t)cs, (uint64_t)cs, mask);
+}

@@ -1,0 +1,352 @@
+// dse_kernels.hip -- gfx950 (MI355X) kernels for the chunked odd-only sieve.
+//
+// Replaces the reference's per-prime serial loop (sieve.clj:118-172:
+// find-next-non-zero -> broadcast [mi ps p] -> mark-composites' lazy index walk
+// with assoc! ... 0) by an LDS-resident segmented sieve. Bit j of a range
+// stands for the odd value 3+2(g_start+j), exactly the reference's element j of
+// its chunk vector (sieve.clj:9-13); a set bit in the output = "element still
+// non-zero" = prime.
+//
+// Per 2^20-candidate segment, one 1024-thread workgroup (one per CU, 128 KiB LDS):
+//   1. zero the LDS segment (ds_write_b128);
+//   2. mark composites with ds_or_b32, work handed out dynamically to waves:
+//      - "mid" primes 61 < p <= LS: one prime per wave, lane L walks its own
+//        column L (a contiguous LS-bit sub-segment stored in LDS bank L mod 32),
+//        so every wave-instruction is bank-conflict-free;
+//      - "large" primes p > LS: one prime per lane, <= SEG/p hits each;
+//   3. write back: lane L reads 4 rows of its column (conflict-free), ORs in the
+//      register patterns of the primes 3..61, inverts, masks the range end,
+//      popcounts, stores 16 B; the block count goes to one 64-bit atomic.
+// See DESIGN.md for the LDS layout and the rooflines.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dse_internal.h"
+
+namespace dse {
+namespace {
+
+constexpr int kNumSmall = 17;
+constexpr uint32_t kSmall[kNumSmall] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61};
+
+constexpr uint64_t pat64(uint32_t q) {
+  uint64_t v = 0;
+  for (uint32_t k = 0; k < 64; k += q) v |= 1ull << k;
+  return v;
+}
+// Bits at the odd indices (q-3)/2 of the small primes themselves: their own
+// pattern marks them, the reference keeps them (they are primes).
+constexpr uint64_t small_self_bits() {
+  uint64_t v = 0;
+  for (int i = 0; i < kNumSmall; ++i) v |= 1ull << ((kSmall[i] - 3) / 2);
+  return v;
+}
+
+__device__ __forceinline__ void lds_or(uint32_t* a, uint32_t v) {
+  __hip_atomic_fetch_or(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// x mod p for x < 2^63 with m = floor((2^64-1)/p).
+__device__ __forceinline__ uint32_t mod_barrett(uint64_t x, uint32_t p, uint64_t m) {
+  uint64_t q = __umul64hi(x, m);
+  uint64_t r = x - q * p;
+  if (r >= p) r -= p;
+  if (r >= p) r -= p;
+  return (uint32_t)r;
+}
+
+// t mod p for t/p < 2^16, t < 2^24, via a float reciprocal and one fix-up.
+__device__ __forceinline__ uint32_t mod_small(uint32_t t, uint32_t p, float invp) {
+  uint32_t q = (uint32_t)((float)t * invp);
+  int32_t r = (int32_t)(t - q * p);
+  r = r < 0 ? r + (int32_t)p : r;
+  r = r >= (int32_t)p ? r - (int32_t)p : r;
+  return (uint32_t)r;
+}
+
+__device__ __forceinline__ uint32_t wave_uniform(uint32_t v) {
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+template <int LOG_SEG, int NT>
+__global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restrict__ table,
+                                                           uint64_t g_start, uint64_t nbits,
+                                                           uint32_t* __restrict__ out,
+                                                           unsigned long long* __restrict__ count_out) {
+  constexpr uint32_t SEG = 1u << LOG_SEG;      // odd candidates per segment
+  constexpr uint32_t LOG_LS = LOG_SEG - 6;
+  constexpr uint32_t LS = 1u << LOG_LS;        // candidates per column (64 columns)
+  constexpr uint32_t ROWS = LS / 32;           // 32-bit words per column
+  constexpr uint32_t NW = NT / 64;
+  constexpr uint32_t ROWS_PER_WAVE = ROWS / NW;
+  static_assert(ROWS_PER_WAVE % 4 == 0, "write-back handles 4 rows per step");
+
+  __shared__ __attribute__((aligned(16))) uint32_t seg[SEG / 32];
+  __shared__ uint32_t s_ctr;
+  __shared__ uint32_t s_thr[2];
+  __shared__ unsigned long long s_wave_cnt[NW];
+
+  const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
+  const uint32_t np = th->count;
+  const uint32_t* __restrict__ P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
+  const uint64_t* __restrict__ M =
+      reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  if (tid == 0) {
+    // first index with p > kSmallMax, first index with p > LS
+    uint32_t lo = 0, hi = np;
+    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= (uint32_t)kSmallMax) lo = mid + 1; else hi = mid; }
+    s_thr[0] = lo;
+    hi = np;
+    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= LS) lo = mid + 1; else hi = mid; }
+    s_thr[1] = lo;
+  }
+  __syncthreads();
+  const uint32_t i_mid0 = s_thr[0], i_mid1 = s_thr[1];
+  const uint32_t n_mid = i_mid1 - i_mid0;
+  const uint32_t n_units = n_mid + (np - i_mid1 + 63) / 64;
+
+  const uint64_t out_words = 2ull * ((nbits + 63) / 64);  // 32-bit words of the caller's mask
+  const uint64_t nseg = (nbits + SEG - 1) / SEG;
+  unsigned long long my_count = 0;
+
+  for (uint64_t s = blockIdx.x; s < nseg; s += gridDim.x) {
+    const uint64_t G = g_start + s * SEG;  // global odd index of segment bit 0
+    const uint64_t seg_end = G + SEG;
+
+    // ---- 1. zero -------------------------------------------------------
+    {
+      uint4* s4 = reinterpret_cast<uint4*>(seg);
+#pragma unroll
+      for (uint32_t i = tid; i < SEG / 128; i += NT) s4[i] = make_uint4(0u, 0u, 0u, 0u);
+      if (tid == 0) s_ctr = 0;
+    }
+    __syncthreads();
+
+    // ---- 2. mark -------------------------------------------------------
+    for (;;) {
+      uint32_t u = 0;
+      if (lane == 0) u = atomicAdd(&s_ctr, 1u);
+      u = wave_uniform(__shfl(u, 0));
+      if (u >= n_units) break;
+      if (u < n_mid) {
+        // one mid prime per wave, lane L = column L
+        const uint32_t i = i_mid0 + u;
+        const uint32_t p = P[i];
+        const uint64_t m = M[i];
+        const uint64_t g0 = ((uint64_t)p * p - 3) >> 1;  // index of p^2
+        if (g0 >= seg_end) break;                        // sorted: nothing later hits
+        const float invp = 1.0f / (float)p;
+        uint32_t off;
+        if (g0 <= G) {
+          const uint32_t A = mod_barrett(G - g0, p, m);  // (G - g0) mod p
+          const uint32_t c = mod_small(LS, p, invp);     // LS mod p
+          const uint32_t d = mod_small(A + lane * c, p, invp);
+          off = d ? p - d : 0;
+        } else {
+          const uint64_t GL = G + (uint64_t)lane * LS;
+          if (g0 >= GL) {
+            const uint64_t t = g0 - GL;
+            off = t >= LS ? LS : (uint32_t)t;
+          } else {
+            const uint32_t d = mod_barrett(GL - g0, p, m);
+            off = d ? p - d : 0;
+          }
+        }
+        uint32_t* col = seg + lane;
+        for (; off < LS; off += p) lds_or(col + ((off >> 5) << 6), 1u << (off & 31));
+      } else {
+        // 64 large primes per wave, one per lane, anywhere in the segment
+        const uint32_t base = i_mid1 + (u - n_mid) * 64;
+        const uint32_t p0 = P[base];
+        if ((((uint64_t)p0 * p0 - 3) >> 1) >= seg_end) break;
+        const uint32_t i = base + lane;
+        if (i < np) {
+          const uint32_t p = P[i];
+          const uint64_t g0 = ((uint64_t)p * p - 3) >> 1;
+          if (g0 < seg_end) {
+            uint32_t b;
+            if (g0 >= G) {
+              b = (uint32_t)(g0 - G);
+            } else {
+              const uint32_t d = mod_barrett(G - g0, p, M[i]);
+              b = d ? p - d : 0;
+            }
+            for (; b < SEG; b += p) {
+              const uint32_t o = b & (LS - 1);
+              lds_or(seg + ((o >> 5) << 6) + (b >> LOG_LS), 1u << (o & 31));
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- 3. write back ---------------------------------------------------
+    {
+      const uint32_t r0 = wave * ROWS_PER_WAVE;
+      const uint32_t w0 = lane * ROWS + r0;               // natural 32-bit word in segment
+      const uint64_t X0 = G + 32ull * w0;                 // global odd index of that word's bit 0
+      // residue of the next multiple of each small prime q, relative to X0:
+      // multiples of q have odd index == (q-3)/2 (mod q)
+      uint32_t res[kNumSmall];
+#pragma unroll
+      for (int k = 0; k < kNumSmall; ++k) {
+        const uint32_t q = kSmall[k];
+        const uint32_t xm = (uint32_t)(X0 % q);
+        const uint32_t cq = (q - 3) / 2;
+        res[k] = (cq + q - xm) % q;
+      }
+      const uint64_t pos0 = s * SEG + 32ull * w0;         // position in the caller's range
+#pragma unroll 2
+      for (uint32_t r = 0; r < ROWS_PER_WAVE; r += 4) {
+        const uint32_t* src = seg + (r0 + r) * 64 + lane;
+        uint64_t lo = (uint64_t)src[0] | ((uint64_t)src[64] << 32);
+        uint64_t hi = (uint64_t)src[128] | ((uint64_t)src[192] << 32);
+#pragma unroll
+        for (int k = 0; k < kNumSmall; ++k) {
+          const uint32_t q = kSmall[k];
+          const uint32_t d64 = 64 % q;
+          uint32_t t = res[k];
+          lo |= pat64(q) << t;
+          t = t >= d64 ? t - d64 : t + q - d64;
+          hi |= pat64(q) << t;
+          t = t >= d64 ? t - d64 : t + q - d64;
+          res[k] = t;
+        }
+        const uint64_t X = X0 + 32ull * r;
+        if (X < 64) lo &= ~(small_self_bits() >> X);
+        lo = ~lo;
+        hi = ~hi;
+        const uint64_t pos = pos0 + 32ull * r;
+        if (pos + 128 > nbits) {
+          lo = pos >= nbits ? 0 : (nbits - pos >= 64 ? lo : lo & ((1ull << (nbits - pos)) - 1));
+          hi = pos + 64 >= nbits ? 0 : (nbits - pos - 64 >= 64 ? hi : hi & ((1ull << (nbits - pos - 64)) - 1));
+        }
+        my_count += (unsigned long long)(__popcll(lo) + __popcll(hi));
+        if (out) {
+          const uint64_t wi = pos >> 5;
+          if (wi + 4 <= out_words) {
+            *reinterpret_cast<uint4*>(out + wi) =
+                make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+          } else {
+            if (wi + 0 < out_words) out[wi + 0] = (uint32_t)lo;
+            if (wi + 1 < out_words) out[wi + 1] = (uint32_t)(lo >> 32);
+            if (wi + 2 < out_words) out[wi + 2] = (uint32_t)hi;
+            if (wi + 3 < out_words) out[wi + 3] = (uint32_t)(hi >> 32);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- block count -> one 64-bit atomic --------------------------------
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) my_count += __shfl_xor(my_count, o);
+  if (lane == 0) s_wave_cnt[wave] = my_count;
+  __syncthreads();
+  if (tid == 0) {
+    unsigned long long t = 0;
+    for (uint32_t w = 0; w < NW; ++w) t += s_wave_cnt[w];
+    if (t) atomicAdd(count_out, t);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Base primes: every odd prime <= limit into the table, one workgroup.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kBaseWords = 150u * 256u;  // 150 KiB of LDS bits (odd values)
+
+__global__ __launch_bounds__(1024) void base_primes_kernel(uint64_t limit, void* __restrict__ table, uint32_t cap) {
+  __shared__ uint32_t bm[kBaseWords];      // 1 = odd index g (value 3+2g) is composite
+  __shared__ uint32_t s_scan[1024];
+  __shared__ uint8_t s_isp[1024];         // primality of the sieving primes q = 3+2t <= sqrt(limit)
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nb = limit >= 3 ? (uint32_t)((limit - 3) / 2 + 1) : 0u;
+  const uint32_t nw = (nb + 31) / 32;
+  for (uint32_t i = tid; i < nw; i += 1024) bm[i] = 0;
+  {
+    const uint32_t q = 3 + 2 * tid;
+    bool pr = (uint64_t)q * q <= limit;
+    for (uint32_t d = 3; pr && d * d <= q; d += 2)
+      if (q % d == 0) pr = false;
+    s_isp[tid] = pr ? 1 : 0;
+  }
+  __syncthreads();
+  for (uint32_t t = 0; t < 1024; ++t) {
+    const uint32_t q = 3 + 2 * t;
+    if ((uint64_t)q * q > limit) break;
+    if (!s_isp[t]) continue;
+    for (uint64_t v = (uint64_t)q * q + 2ull * q * tid; v <= limit; v += 2ull * q * 1024) {
+      const uint32_t g = (uint32_t)((v - 3) >> 1);
+      __hip_atomic_fetch_or(&bm[g >> 5], 1u << (g & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  __syncthreads();
+  // ordered compaction: thread t owns words [t*wpt, (t+1)*wpt)
+  const uint32_t wpt = (nw + 1023) / 1024;
+  const uint32_t wb = tid * wpt, we = min(nw, wb + wpt);
+  uint32_t cnt = 0;
+  for (uint32_t w = wb; w < we; ++w) {
+    uint32_t v = ~bm[w];
+    if (w == nw - 1 && (nb & 31)) v &= (1u << (nb & 31)) - 1;
+    cnt += __popc(v);
+  }
+  s_scan[tid] = cnt;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
+    uint32_t x = tid >= o ? s_scan[tid - o] : 0;
+    __syncthreads();
+    s_scan[tid] += x;
+    __syncthreads();
+  }
+  const uint32_t total = s_scan[1023];
+  uint32_t pos = s_scan[tid] - cnt;
+  uint32_t* Pout = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + 16);
+  uint64_t* Mout = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(table) + table_m_offset(cap));
+  if (total <= cap) {
+    for (uint32_t w = wb; w < we; ++w) {
+      uint32_t v = ~bm[w];
+      if (w == nw - 1 && (nb & 31)) v &= (1u << (nb & 31)) - 1;
+      while (v) {
+        const uint32_t b = __ffs(v) - 1;
+        v &= v - 1;
+        const uint32_t p = 3 + 2 * (w * 32 + b);
+        Pout[pos] = p;
+        Mout[pos] = ~0ull / p;
+        ++pos;
+      }
+    }
+  }
+  if (tid == 0) {
+    TableHeader* h = reinterpret_cast<TableHeader*>(table);
+    h->count = total <= cap ? total : 0xFFFFFFFFu;
+    h->cap = cap;
+    h->limit = limit;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_base_primes(uint64_t limit, void* table, uint32_t cap, hipStream_t stream) {
+  if (limit > kBaseLimitMax) return hipErrorInvalidValue;
+  if (limit > 2ull * 32ull * kBaseWords + 1ull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(base_primes_kernel, dim3(1), dim3(1024), 0, stream, limit, table, cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
+                              unsigned long long* count, int num_cus, hipStream_t stream) {
+  if (nbits == 0) return hipSuccess;
+  constexpr uint64_t SEG = 1ull << kLogSeg;
+  const uint64_t nseg = (nbits + SEG - 1) / SEG;
+  const uint64_t grid = nseg < (uint64_t)num_cus ? nseg : (uint64_t)num_cus;
+  hipLaunchKernelGGL((sieve_segments_kernel<kLogSeg, kThreads>), dim3((uint32_t)grid), dim3(kThreads), 0,
+                     stream, table, g_start, nbits, out, count);
+  return hipGetLastError();
+}
+
+}  // namespace dse

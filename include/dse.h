@@ -1,0 +1,156 @@
+/*
+ * dse.h -- C ABI of the MI355X-native chunked odd-only sieve (libdse.so).
+ *
+ * This is the drop-in boundary for the hot path of dpbriggs/Distributed-Sieve-e:
+ * the reference's lead/follower entry points (core.clj:136-205) call
+ * spread-work / gen-table / sieve-e / finish (sieve.clj:9-172); here those
+ * calls become the functions below, which launch hand-written gfx950 HIP
+ * kernels. Each declaration names the reference interface it replaces.
+ *
+ * Conventions
+ *  - Every function returns DSE_OK (0) or a negative DSE_E* status; the
+ *    message of the last failure on the calling thread is dse_last_error().
+ *  - Host output buffers are caller-allocated (ctypes / JNA Memory / FFM
+ *    MemorySegment). The library never retains caller pointers.
+ *  - Device buffers are owned by the dse_ctx, except in the *_dev entry
+ *    points, which take caller-owned device pointers (e.g. torch tensors).
+ *  - Calls are blocking (like sieve-e on the caller's main thread,
+ *    core.clj:163,196) unless the name ends in _async.
+ *  - Chunk semantics are the reference's exactly: cs = floor(floor((n-1)/2)/P),
+ *    chunk k (1-based) holds the odd values [3+2(k-1)cs, 3+2k*cs); the
+ *    floor((n-1)/2) - P*cs highest odd candidates are dropped (sieve.clj:21-34).
+ *  - Mask layout: little-endian uint64 words, bit j of chunk k = 1 iff the
+ *    value 3+2((k-1)cs+j) is prime (= element j non-zero before finish);
+ *    bits past cs in the last word are 0.
+ */
+#ifndef DSE_H
+#define DSE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DSE_OK 0
+#define DSE_EINVAL -1   /* bad argument (P < 1, cs < 4 where finish needs it, ...) */
+#define DSE_EHIP -2     /* HIP runtime error */
+#define DSE_ENCCL -3    /* RCCL error */
+#define DSE_ENOMEM -4   /* host or device allocation failed */
+#define DSE_EIO -5      /* file I/O */
+#define DSE_ERANGE -6   /* input outside the supported range */
+
+typedef struct dse_ctx dse_ctx;
+
+/* Library version string, e.g. "dse 0.1 gfx950". */
+const char *dse_version(void);
+
+/* Message of the last failed call on this thread ("" if none). */
+const char *dse_last_error(void);
+
+/* Number of visible HIP devices (0 if none). */
+int32_t dse_device_count(void);
+
+/* One process driving num_gpus devices 0..num_gpus-1 (0 = all visible), with
+ * one RCCL communicator over them when num_gpus > 1. Replaces the lead's
+ * socket server + client wait (core.clj:76-116, 141-147). NULL on failure. */
+dse_ctx *dse_init(int32_t num_gpus);
+
+/* One context bound to a single device, for one-process-per-GPU ranks that
+ * bring their own communicator (torch.distributed / RCCL). Replaces the
+ * follower's connect (core.clj:13-31, 186). NULL on failure. */
+dse_ctx *dse_init_device(int32_t device);
+
+void dse_destroy(dse_ctx *ctx);
+
+/* Number of devices the context drives. */
+int32_t dse_ctx_num_devices(const dse_ctx *ctx);
+
+/* sieve.clj:15-34 spread-work, in exact int64: lo_hi[2(k-1)], lo_hi[2(k-1)+1]
+ * = bounds of chunk k (caller allocates 2*P entries; may be NULL); *cs = chunk
+ * size in odd candidates. */
+int32_t dse_spread_work(int64_t n, int32_t P, int64_t *lo_hi, int64_t *cs);
+
+/* Odd indices [*g_start, *g_start + *nbits) that spread-work drops
+ * (values 3+2P*cs .. n); *nbits <= P-1. */
+int32_t dse_tail_range(int64_t n, int32_t P, uint64_t *g_start, uint64_t *nbits);
+
+/* gen-table + sieve-e for ONE chunk (sieve.clj:9-13, 118-172; core.clj:152,
+ * 163, 192, 196): sieve chunk my_num of the (n, P) run on the context's
+ * device ((my_num-1) mod num_devices). mask_or_null: host buffer of
+ * ceil(cs/64) uint64 words, or NULL for count only. *count = primes in the
+ * chunk (odd values only; the "2" that finish injects is not counted). */
+int32_t dse_sieve_chunk(dse_ctx *ctx, int64_t n, int32_t P, int32_t my_num,
+                        uint64_t *mask_or_null, uint64_t *count);
+
+/* gen-table + sieve-e for an arbitrary odd-index range (a chunk given by its
+ * bounds [lo, hi): g_start = (lo-3)/2, nbits = (hi-lo)/2), on the context's
+ * first device. mask_or_null: ceil(nbits/64) words; *count = primes. */
+int32_t dse_sieve_odd_range(dse_ctx *ctx, uint64_t g_start, uint64_t nbits,
+                            uint64_t *mask_or_null, uint64_t *count);
+
+/* The whole lead/follower run (core.clj:136-205) on the context's devices:
+ * base primes <= sqrt(max value) computed once on device 0 and broadcast with
+ * RCCL (replaces the per-prime [mi ps p] relay, sieve.clj:139 /
+ * core.clj:118-134), chunk k sieved on device (k-1) mod num_devices with its
+ * mask left resident in that device's HBM, the dropped tail sieved on the last
+ * device, counts combined with an RCCL all-reduce.
+ * per_chunk_counts: P entries (may be NULL). *pi_ref = 1 + sum(counts) (what
+ * the reference's files hold); *pi_full = pi_ref + primes in the tail = pi(n).
+ * Either pi pointer may be NULL. */
+int32_t dse_sieve_all(dse_ctx *ctx, int64_t n, int32_t P, uint64_t *per_chunk_counts,
+                      uint64_t *pi_ref, uint64_t *pi_full);
+
+/* Copy chunk my_num's mask kept resident by the last dse_sieve_all into a host
+ * buffer of ceil(cs/64) words. DSE_EINVAL if that chunk is not resident. */
+int32_t dse_copy_chunk_mask(dse_ctx *ctx, int32_t my_num, uint64_t *mask);
+
+/* Sieve the odd values in [lo, hi] (any 64-bit window, lo,hi odd or even;
+ * "segment-only" mode outside the reference's chunk semantics). Counts
+ * primes in [max(lo,3), hi] among odd values. */
+int32_t dse_sieve_window(dse_ctx *ctx, uint64_t lo, uint64_t hi, uint64_t *count);
+
+/* sieve.clj:82-108 finish: write chunk my_num's primes to path, byte-exact
+ * with the reference's file: chunk 1 values printed as Java Doubles ("2.0",
+ * "1.0000019E7") with the 2/3/5/7 hack, others as Longs; 10 per line,
+ * ", "-separated, LF-terminated lines. mask: ceil(cs/64) words. Needs cs >= 4. */
+int32_t dse_write_primes_file(const char *path, int32_t my_num, int64_t n, int32_t P,
+                              const uint64_t *mask);
+
+/* finish for a chunk given by its odd-index range: same format as
+ * dse_write_primes_file; my_num == 1 selects the Double printing + hack. */
+int32_t dse_write_range_file(const char *path, int32_t my_num, uint64_t g_start, uint64_t nbits,
+                             const uint64_t *mask);
+
+/* ---- Device-resident entry points (one-process-per-GPU ranks) ---------- */
+
+/* Bytes of a base-prime table able to hold every odd prime <= limit. */
+uint64_t dse_base_table_bytes(uint64_t limit);
+
+/* Largest base-prime limit the device kernel supports. */
+uint64_t dse_base_limit_max(void);
+
+/* isqrt of the largest value in odd-index range [g_start, g_start+nbits):
+ * the base-prime limit that range needs. */
+uint64_t dse_base_limit_for_range(uint64_t g_start, uint64_t nbits);
+
+/* Build the table of odd primes <= limit into caller-owned device memory
+ * table_dev (dse_base_table_bytes(limit) bytes) on stream (hipStream_t, NULL
+ * = default). Asynchronous. The table is plain bytes: ranks may broadcast it
+ * with any collective (RCCL) before sieving. */
+int32_t dse_base_primes_dev_async(dse_ctx *ctx, uint64_t limit, void *table_dev,
+                                  uint64_t table_bytes, void *stream);
+
+/* Sieve odd indices [g_start, g_start+nbits) with a base table on the device:
+ * mask_dev (ceil(nbits/64) uint64 words, or NULL) receives the prime bits,
+ * *count_dev (device uint64) is INCREMENTED by the prime count (zero it
+ * first). Asynchronous on stream. */
+int32_t dse_sieve_range_dev_async(dse_ctx *ctx, const void *table_dev, uint64_t g_start,
+                                  uint64_t nbits, uint64_t *mask_dev, uint64_t *count_dev,
+                                  void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DSE_H */
