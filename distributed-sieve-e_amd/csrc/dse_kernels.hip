@@ -68,6 +68,57 @@ __device__ __forceinline__ uint32_t wave_uniform(uint32_t v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
+// Per-column marking of one mid prime (p <= LS) in the fast case (p^2 at or
+// before the segment): lane L = column L starts at the first multiple at or
+// after G + L*LS. A = (G - g0) mod p, c = LS mod p (both wave-uniform).
+template <uint32_t LS>
+__device__ __forceinline__ void mark_column(uint32_t* __restrict__ col, uint32_t lane, uint32_t p, uint32_t A,
+                                            uint32_t c, float invp) {
+  const uint32_t d = mod_small(A + lane * c, p, invp);  // (G + L*LS - g0) mod p
+  uint32_t off = d ? p - d : 0;
+  // every lane has floor(LS/p) hits, some one more: uniform loop + one predicated
+  const uint32_t n_full = (uint32_t)((float)(LS - c) * invp + 0.5f);
+#pragma unroll 4
+  for (uint32_t k = 0; k < n_full; ++k) {
+    lds_or(col + ((off >> 5) << 6), 1u << (off & 31));
+    off += p;
+  }
+  if (off < LS) lds_or(col + ((off >> 5) << 6), 1u << (off & 31));
+}
+
+// Slow case (p^2 inside or after this segment's start): per-lane offsets.
+template <uint32_t LS>
+__device__ __forceinline__ void mark_column_slow(uint32_t* __restrict__ col, uint32_t lane, uint32_t p, uint64_t m,
+                                                 uint64_t g0, uint64_t G) {
+  const uint64_t GL = G + (uint64_t)lane * LS;
+  uint32_t off;
+  if (g0 >= GL) {
+    const uint64_t t = g0 - GL;
+    off = t >= LS ? LS : (uint32_t)t;
+  } else {
+    const uint32_t d = mod_barrett(GL - g0, p, m);
+    off = d ? p - d : 0;
+  }
+  for (; off < LS; off += p) lds_or(col + ((off >> 5) << 6), 1u << (off & 31));
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+  return wave_uniform(v);
+}
+
+// floor(t / p) for t < 2^24 via a float reciprocal, corrected.
+__device__ __forceinline__ uint32_t div_small(uint32_t t, uint32_t p, float invp) {
+  uint32_t q = (uint32_t)((float)t * invp);
+  const uint32_t qp = q * p;
+  q = qp > t ? q - 1 : q;
+  q = (q + 1) * p <= t ? q + 1 : q;
+  return q;
+}
+
+constexpr uint32_t kMaxMid = 1920;  // mid primes staged in LDS (odd primes 67..16384: 1882)
+
 template <int LOG_SEG, int NT>
 __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restrict__ table,
                                                            uint64_t g_start, uint64_t nbits,
@@ -79,11 +130,14 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
   constexpr uint32_t ROWS = LS / 32;           // 32-bit words per column
   constexpr uint32_t NW = NT / 64;
   constexpr uint32_t ROWS_PER_WAVE = ROWS / NW;
+  constexpr uint32_t TA = LS / 16;             // mid primes <= TA: one per grab (>= 16 hits per column)
   static_assert(ROWS_PER_WAVE % 4 == 0, "write-back handles 4 rows per step");
 
   __shared__ __attribute__((aligned(16))) uint32_t seg[SEG / 32];
+  __shared__ uint64_t s_mid_m[kMaxMid];
+  __shared__ uint32_t s_mid_p[kMaxMid];
   __shared__ uint32_t s_ctr;
-  __shared__ uint32_t s_thr[2];
+  __shared__ uint32_t s_thr[3];
   __shared__ unsigned long long s_wave_cnt[NW];
 
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
@@ -95,22 +149,34 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
   if (tid == 0) {
-    // first index with p > kSmallMax, first index with p > LS
+    // first index with p > kSmallMax, with p > TA, with p > LS
     uint32_t lo = 0, hi = np;
     while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= (uint32_t)kSmallMax) lo = mid + 1; else hi = mid; }
     s_thr[0] = lo;
     hi = np;
-    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= LS) lo = mid + 1; else hi = mid; }
+    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= TA) lo = mid + 1; else hi = mid; }
     s_thr[1] = lo;
+    hi = np;
+    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= LS) lo = mid + 1; else hi = mid; }
+    s_thr[2] = min(lo, s_thr[0] + kMaxMid);  // anything beyond the LDS stage goes to the large path
   }
   __syncthreads();
-  const uint32_t i_mid0 = s_thr[0], i_mid1 = s_thr[1];
-  const uint32_t n_mid = i_mid1 - i_mid0;
-  const uint32_t n_units = n_mid + (np - i_mid1 + 63) / 64;
+  const uint32_t i_mid0 = s_thr[0], i_midA = s_thr[1], i_mid1 = s_thr[2];
+  for (uint32_t i = tid; i < i_mid1 - i_mid0; i += NT) {
+    s_mid_p[i] = P[i_mid0 + i];
+    s_mid_m[i] = M[i_mid0 + i];
+  }
+  // unit space: [0,nA) single mid primes <= TA; [nA, nA+nB) batches of 64 mid
+  // primes; [.., +nC) batches of 64 large primes (one per lane)
+  const uint32_t nA = i_midA - i_mid0;
+  const uint32_t nB = (i_mid1 - i_midA + 63) / 64;
+  const uint32_t nC = (np - i_mid1 + 63) / 64;
+  const uint32_t n_units = nA + nB + nC;
 
   const uint64_t out_words = 2ull * ((nbits + 63) / 64);  // 32-bit words of the caller's mask
   const uint64_t nseg = (nbits + SEG - 1) / SEG;
   unsigned long long my_count = 0;
+  uint32_t* const col = seg + lane;
 
   for (uint64_t s = blockIdx.x; s < nseg; s += gridDim.x) {
     const uint64_t G = g_start + s * SEG;  // global odd index of segment bit 0
@@ -131,54 +197,77 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
       if (lane == 0) u = atomicAdd(&s_ctr, 1u);
       u = wave_uniform(__shfl(u, 0));
       if (u >= n_units) break;
-      if (u < n_mid) {
-        // one mid prime per wave, lane L = column L
-        const uint32_t i = i_mid0 + u;
-        const uint32_t p = P[i];
-        const uint64_t m = M[i];
+      if (u < nA) {
+        // one mid prime (p <= TA) for the whole wave
+        const uint32_t p = s_mid_p[u];
+        const uint64_t m = s_mid_m[u];
         const uint64_t g0 = ((uint64_t)p * p - 3) >> 1;  // index of p^2
         if (g0 >= seg_end) break;                        // sorted: nothing later hits
-        const float invp = 1.0f / (float)p;
-        uint32_t off;
         if (g0 <= G) {
-          const uint32_t A = mod_barrett(G - g0, p, m);  // (G - g0) mod p
-          const uint32_t c = mod_small(LS, p, invp);     // LS mod p
-          const uint32_t d = mod_small(A + lane * c, p, invp);
-          off = d ? p - d : 0;
+          const float invp = 1.0f / (float)p;
+          mark_column<LS>(col, lane, p, mod_barrett(G - g0, p, m), mod_small(LS, p, invp), invp);
         } else {
-          const uint64_t GL = G + (uint64_t)lane * LS;
-          if (g0 >= GL) {
-            const uint64_t t = g0 - GL;
-            off = t >= LS ? LS : (uint32_t)t;
+          mark_column_slow<LS>(col, lane, p, m, g0, G);
+        }
+      } else if (u < nA + nB) {
+        // 64 mid primes: per-lane setup, then one prime at a time for the wave
+        const uint32_t j0 = nA + (u - nA) * 64;
+        const uint32_t jl = j0 + lane;
+        const bool valid = jl < i_mid1 - i_mid0;
+        const uint32_t pl = valid ? s_mid_p[jl] : 0xFFFFFFFFu;
+        const uint64_t ml = valid ? s_mid_m[jl] : 1;
+        const uint64_t g0l = valid ? (((uint64_t)pl * pl - 3) >> 1) : ~0ull;
+        if (wave_uniform((uint32_t)(((uint64_t)s_mid_p[j0] * s_mid_p[j0] - 3) >> 1 >= seg_end))) break;
+        const bool fast = g0l <= G;
+        const float invpl = 1.0f / (float)pl;
+        const uint32_t Al = fast ? mod_barrett(G - g0l, pl, ml) : 0;
+        const uint32_t cl = mod_small(LS, pl, invpl);
+        const uint32_t nj = min(64u, (i_mid1 - i_mid0) - j0);
+        for (uint32_t j = 0; j < nj; ++j) {
+          const uint32_t p = __builtin_amdgcn_readlane(pl, j);
+          const uint64_t g0 = ((uint64_t)p * p - 3) >> 1;
+          if (g0 >= seg_end) break;
+          if (g0 <= G) {
+            const uint32_t A = __builtin_amdgcn_readlane(Al, j);
+            const uint32_t c = __builtin_amdgcn_readlane(cl, j);
+            const float invp = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(invpl), j));
+            mark_column<LS>(col, lane, p, A, c, invp);
           } else {
-            const uint32_t d = mod_barrett(GL - g0, p, m);
-            off = d ? p - d : 0;
+            mark_column_slow<LS>(col, lane, p, s_mid_m[j0 + j], g0, G);
           }
         }
-        uint32_t* col = seg + lane;
-        for (; off < LS; off += p) lds_or(col + ((off >> 5) << 6), 1u << (off & 31));
       } else {
         // 64 large primes per wave, one per lane, anywhere in the segment
-        const uint32_t base = i_mid1 + (u - n_mid) * 64;
+        const uint32_t base = i_mid1 + (u - nA - nB) * 64;
         const uint32_t p0 = P[base];
         if ((((uint64_t)p0 * p0 - 3) >> 1) >= seg_end) break;
         const uint32_t i = base + lane;
+        uint32_t b = SEG, p = 1;
         if (i < np) {
-          const uint32_t p = P[i];
+          p = P[i];
           const uint64_t g0 = ((uint64_t)p * p - 3) >> 1;
           if (g0 < seg_end) {
-            uint32_t b;
             if (g0 >= G) {
               b = (uint32_t)(g0 - G);
             } else {
               const uint32_t d = mod_barrett(G - g0, p, M[i]);
               b = d ? p - d : 0;
             }
-            for (; b < SEG; b += p) {
-              const uint32_t o = b & (LS - 1);
-              lds_or(seg + ((o >> 5) << 6) + (b >> LOG_LS), 1u << (o & 31));
-            }
           }
+        }
+        // hits per lane differ little between neighbouring primes: run the
+        // wave-wide minimum without exec-mask churn, then the remainder
+        const uint32_t trips = b < SEG ? div_small(SEG - 1 - b, p, 1.0f / (float)p) + 1 : 0;
+        const uint32_t n_min = wave_min_u32(trips);
+#pragma unroll 2
+        for (uint32_t k = 0; k < n_min; ++k) {
+          const uint32_t o = b & (LS - 1);
+          lds_or(seg + ((o >> 5) << 6) + (b >> LOG_LS), 1u << (o & 31));
+          b += p;
+        }
+        for (; b < SEG; b += p) {
+          const uint32_t o = b & (LS - 1);
+          lds_or(seg + ((o >> 5) << 6) + (b >> LOG_LS), 1u << (o & 31));
         }
       }
     }

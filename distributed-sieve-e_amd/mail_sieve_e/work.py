@@ -1,0 +1,72 @@
+"""Algorithmic work of the sieve, for roofline accounting.
+
+marks(range) = sum over odd primes p <= sqrt(max value) of the number of odd
+multiples of p in [max(p^2, lo), hi]; an LDS-resident sieve pays one 4-byte
+LDS read + one 4-byte write per mark (8 B/mark), and writes
+the mask (nbits/8 bytes) to HBM once.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md): 256 CUs at 2.4 GHz,
+# LDS 128 B/clk/CU for 4-byte-per-lane access (ds_read_b32 row of the LDS
+# table; "~75 TB/s for ds_read_b32" aggregate), HBM3E 8 TB/s spec.
+NUM_CUS = 256
+CLOCK_HZ = 2.4e9
+LDS_PEAK_GBS = NUM_CUS * 128 * CLOCK_HZ / 1e9      # 78,643 GB/s
+HBM_PEAK_GBS = 8000.0
+BYTES_PER_MARK = 8
+
+
+def odd_primes_upto(x: int) -> np.ndarray:
+    if x < 3:
+        return np.zeros(0, dtype=np.int64)
+    s = np.ones(x // 2 + 1, dtype=bool)  # s[i] <-> 2i+1
+    s[0] = False
+    for i in range(1, (math.isqrt(x) - 1) // 2 + 1):
+        if s[i]:
+            p = 2 * i + 1
+            s[p * p // 2::p] = False
+    return (2 * np.flatnonzero(s) + 1).astype(np.int64)
+
+
+def marks_for_range(g_start: int, nbits: int) -> int:
+    """Odd multiples >= p^2 of every odd prime p <= sqrt(vmax) that fall in
+    the odd-index range [g_start, g_start+nbits) (values 3+2g)."""
+    if nbits <= 0:
+        return 0
+    va = 3 + 2 * g_start
+    vb = 3 + 2 * (g_start + nbits - 1)
+    ps = odd_primes_upto(math.isqrt(vb))
+    if ps.size == 0:
+        return 0
+    lo = np.maximum(ps * ps, va)
+    m0 = (lo + ps - 1) // ps
+    m0 += (m0 % 2 == 0)
+    m1 = vb // ps
+    m1 -= (m1 % 2 == 0)
+    cnt = np.where(m1 >= m0, (m1 - m0) // 2 + 1, 0)
+    return int(cnt.sum())
+
+
+def roofline(g_start: int, nbits: int, seconds: float, launches: int = 1) -> dict:
+    """t_roof = max(8*marks/BW_LDS, (nbits/8)/BW_HBM)."""
+    marks = marks_for_range(g_start, nbits)
+    lds_bytes = BYTES_PER_MARK * marks
+    hbm_bytes = (nbits + 7) // 8
+    t = seconds / launches
+    t_lds = lds_bytes / (LDS_PEAK_GBS * 1e9)
+    t_hbm = hbm_bytes / (HBM_PEAK_GBS * 1e9)
+    return {
+        "marks": marks,
+        "lds_bytes": lds_bytes,
+        "hbm_bytes": hbm_bytes,
+        "t_roof_s": max(t_lds, t_hbm),
+        "bound": "lds" if t_lds >= t_hbm else "hbm",
+        "lds_achieved_gbs": lds_bytes / t / 1e9,
+        "hbm_achieved_gbs": hbm_bytes / t / 1e9,
+        "frac": max(t_lds, t_hbm) / t,
+    }

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Profile bench.py on the GPU box: kernel trace + stats, then PMC passes
+# (one block-limited counter group per run, never combined with tracing).
+# Usage (via gpurun): bash tools/profile.sh <tag> [bench args...]
+set -u
+TAG=${1:-r01}; shift || true
+ARGS=${*:---steps 5 --warmup 2 --cpu-baseline off}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+run() {  # name, rocprof args...
+  local name=$1; shift
+  timeout -k 10 180 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 bench.py $ARGS \
+    > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "[$name] rc=$rc"
+  return $rc
+}
+run trace --kernel-trace --stats || exit 1
+run pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE || exit 1
+run pmc_wait --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT || exit 1
+run pmc_fetch --pmc FETCH_SIZE || exit 1
+run pmc_write --pmc WRITE_SIZE || exit 1
+echo done
