@@ -20,11 +20,15 @@
 // See DESIGN.md for the LDS layout and the rooflines.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "dse_internal.h"
 
 namespace dse {
 namespace {
+
+constexpr uint32_t kPhaseMidA = 1, kPhaseMidB = 2, kPhaseLarge = 4, kPhaseSmall = 8, kPhaseStore = 16;
+constexpr uint32_t kPhaseAll = 31;
 
 constexpr int kNumSmall = 17;
 constexpr uint32_t kSmall[kNumSmall] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61};
@@ -123,7 +127,8 @@ template <int LOG_SEG, int NT>
 __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restrict__ table,
                                                            uint64_t g_start, uint64_t nbits,
                                                            uint32_t* __restrict__ out,
-                                                           unsigned long long* __restrict__ count_out) {
+                                                           unsigned long long* __restrict__ count_out,
+                                                           uint32_t phases) {
   constexpr uint32_t SEG = 1u << LOG_SEG;      // odd candidates per segment
   constexpr uint32_t LOG_LS = LOG_SEG - 6;
   constexpr uint32_t LS = 1u << LOG_LS;        // candidates per column (64 columns)
@@ -137,7 +142,7 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
   __shared__ uint64_t s_mid_m[kMaxMid];
   __shared__ uint32_t s_mid_p[kMaxMid];
   __shared__ uint32_t s_ctr;
-  __shared__ uint32_t s_thr[3];
+  __shared__ uint32_t s_thr[4];
   __shared__ unsigned long long s_wave_cnt[NW];
 
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
@@ -159,6 +164,10 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
     hi = np;
     while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= LS) lo = mid + 1; else hi = mid; }
     s_thr[2] = min(lo, s_thr[0] + kMaxMid);  // anything beyond the LDS stage goes to the large path
+    lo = s_thr[2];
+    hi = np;
+    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= 4 * LS) lo = mid + 1; else hi = mid; }
+    s_thr[3] = lo;
   }
   __syncthreads();
   const uint32_t i_mid0 = s_thr[0], i_midA = s_thr[1], i_mid1 = s_thr[2];
@@ -166,17 +175,28 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
     s_mid_p[i] = P[i_mid0 + i];
     s_mid_m[i] = M[i_mid0 + i];
   }
-  // unit space: [0,nA) single mid primes <= TA; [nA, nA+nB) batches of 64 mid
-  // primes; [.., +nC) batches of 64 large primes (one per lane)
+  // Work units, handed out dynamically. S1 = LDS-issue-bound: nA single mid
+  // primes (p <= TA, one per wave), then nB diagonal units (64 mid primes x 16
+  // columns). S2 = large primes: nC cooperative units (64 primes in (LS, 4LS],
+  // a lane per hit), then nD scatter units (256 primes > 4LS, 4 per lane).
+  // S1 and S2 are interleaved so that waves waiting on global loads overlap
+  // waves marking.
+  const uint32_t i_big = s_thr[3];
   const uint32_t nA = i_midA - i_mid0;
-  const uint32_t nB = (i_mid1 - i_midA + 63) / 64;
-  const uint32_t nC = (np - i_mid1 + 63) / 64;
-  const uint32_t n_units = nA + nB + nC;
+  const uint32_t nBb = (i_mid1 - i_midA + 63) / 64;  // batches of 64
+  const uint32_t nB = nBb * 4;                       // x 4 column quarters
+  const uint32_t nC = (i_big - i_mid1 + 63) / 64;
+  const uint32_t nD = (np - i_big + 255) / 256;
+  const uint32_t nS1 = nA + nB, nS2 = nC + nD;
+  const uint32_t nI = min(nS1, nS2);  // interleaved pairs
+  const uint32_t n_units = nS1 + nS2;
+  const uint32_t n_mid = i_mid1 - i_mid0;
 
   const uint64_t out_words = 2ull * ((nbits + 63) / 64);  // 32-bit words of the caller's mask
   const uint64_t nseg = (nbits + SEG - 1) / SEG;
   unsigned long long my_count = 0;
   uint32_t* const col = seg + lane;
+  char* const segb = reinterpret_cast<char*>(seg);
 
   for (uint64_t s = blockIdx.x; s < nseg; s += gridDim.x) {
     const uint64_t G = g_start + s * SEG;  // global odd index of segment bit 0
@@ -197,77 +217,158 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
       if (lane == 0) u = atomicAdd(&s_ctr, 1u);
       u = wave_uniform(__shfl(u, 0));
       if (u >= n_units) break;
-      if (u < nA) {
-        // one mid prime (p <= TA) for the whole wave
-        const uint32_t p = s_mid_p[u];
-        const uint64_t m = s_mid_m[u];
+      // map u -> (list, index)
+      bool in_s1;
+      uint32_t k;
+      if (u < 2 * nI) { in_s1 = !(u & 1); k = u >> 1; }
+      else { in_s1 = nS1 > nS2; k = u - nI; }
+      if (in_s1 && k < nA) {
+        if (!(phases & kPhaseMidA)) continue;
+        // one mid prime (p <= TA) for the whole wave, lane L = column L
+        const uint32_t p = s_mid_p[k];
+        const uint64_t m = s_mid_m[k];
         const uint64_t g0 = ((uint64_t)p * p - 3) >> 1;  // index of p^2
-        if (g0 >= seg_end) break;                        // sorted: nothing later hits
+        if (g0 >= seg_end) continue;
         if (g0 <= G) {
           const float invp = 1.0f / (float)p;
           mark_column<LS>(col, lane, p, mod_barrett(G - g0, p, m), mod_small(LS, p, invp), invp);
         } else {
           mark_column_slow<LS>(col, lane, p, m, g0, G);
         }
-      } else if (u < nA + nB) {
-        // 64 mid primes: per-lane setup, then one prime at a time for the wave
-        const uint32_t j0 = nA + (u - nA) * 64;
-        const uint32_t jl = j0 + lane;
-        const bool valid = jl < i_mid1 - i_mid0;
-        const uint32_t pl = valid ? s_mid_p[jl] : 0xFFFFFFFFu;
-        const uint64_t ml = valid ? s_mid_m[jl] : 1;
-        const uint64_t g0l = valid ? (((uint64_t)pl * pl - 3) >> 1) : ~0ull;
-        if (wave_uniform((uint32_t)(((uint64_t)s_mid_p[j0] * s_mid_p[j0] - 3) >> 1 >= seg_end))) break;
-        const bool fast = g0l <= G;
-        const float invpl = 1.0f / (float)pl;
-        const uint32_t Al = fast ? mod_barrett(G - g0l, pl, ml) : 0;
-        const uint32_t cl = mod_small(LS, pl, invpl);
-        const uint32_t nj = min(64u, (i_mid1 - i_mid0) - j0);
-        for (uint32_t j = 0; j < nj; ++j) {
-          const uint32_t p = __builtin_amdgcn_readlane(pl, j);
+      } else if (in_s1) {
+        if (!(phases & kPhaseMidB)) continue;
+        // 64 mid primes x 16 columns, lane j = prime j, walked diagonally: at
+        // step t lane j is in column (j+16q+t) mod 64, so every ds_or hits a
+        // distinct column (bank = column mod 32) and the column-to-column
+        // hand-over of the offset is free.
+        const uint32_t kb = k - nA, q = kb & 3;
+        const uint32_t j0 = nA + (kb >> 2) * 64;
+        const uint32_t nj = min(64u, n_mid - j0);
+        if ((((uint64_t)s_mid_p[j0] * s_mid_p[j0] - 3) >> 1) >= seg_end) continue;
+        const bool valid = lane < nj;
+        const uint32_t p = valid ? s_mid_p[j0 + lane] : 0x7FFFFFFFu;
+        uint32_t O0 = SEG;  // first hit at or after G, relative to G (SEG: none)
+        if (valid) {
           const uint64_t g0 = ((uint64_t)p * p - 3) >> 1;
-          if (g0 >= seg_end) break;
           if (g0 <= G) {
-            const uint32_t A = __builtin_amdgcn_readlane(Al, j);
-            const uint32_t c = __builtin_amdgcn_readlane(cl, j);
-            const float invp = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(invpl), j));
-            mark_column<LS>(col, lane, p, A, c, invp);
-          } else {
-            mark_column_slow<LS>(col, lane, p, s_mid_m[j0 + j], g0, G);
+            const uint32_t A = mod_barrett(G - g0, p, s_mid_m[j0 + lane]);
+            O0 = A ? p - A : 0;
+          } else if (g0 < seg_end) {
+            O0 = (uint32_t)(g0 - G);
+          }
+        }
+        const float invp = 1.0f / (float)p;
+        const uint32_t c0 = (lane + 16 * q) & 63;
+        const uint32_t cstart = c0 * LS;
+        uint32_t off;
+        if (O0 >= cstart) off = O0 - cstart;
+        else { const uint32_t d = mod_small(cstart - O0, p, invp); off = d ? p - d : 0; }
+        // a lane past p^2 with off < p has floor(LS/p)..ceil(LS/p) hits per
+        // column: n_u unconditional marks + n_x value-predicated ones (OR 0)
+        const uint32_t pmin = __builtin_amdgcn_readlane(p, 0);
+        const uint32_t pmax = __builtin_amdgcn_readlane(p, nj - 1);
+        const bool any_slow = __builtin_amdgcn_ballot_w64(valid && O0 >= p) != 0;
+        const uint32_t n_u = any_slow ? 0u : LS / pmax;
+        const uint32_t n_x = (LS + pmin - 1) / pmin - n_u;
+        uint32_t c4 = c0 << 2;  // byte offset of the current column
+        if (!valid) off = 0x40000000u;  // no marks: every predicated OR is 0
+        for (uint32_t t = 0; t < 16; ++t) {
+#pragma unroll 2
+          for (uint32_t h = 0; h < n_u; ++h) {
+            lds_or(reinterpret_cast<uint32_t*>(segb + (((off >> 5) << 8) | c4)), 1u << (off & 31));
+            off += p;
+          }
+          for (uint32_t h = 0; h < n_x; ++h) {
+            const bool hit = off < LS;
+            const uint32_t o = hit ? off : 0u;
+            lds_or(reinterpret_cast<uint32_t*>(segb + (((o >> 5) << 8) | c4)), hit ? 1u << (o & 31) : 0u);
+            off = hit ? off + p : off;
+          }
+          off -= LS;
+          c4 = (c4 + 4) & 255;
+          off = (c4 == 0 && valid) ? O0 : off;  // wrapped from column 63 to column 0
+        }
+      } else if (k < nC) {
+        if (!(phases & kPhaseLarge)) continue;
+        // 64 primes in (LS, 4LS]: < 64 hits each per segment, at most one per
+        // column. One prime per wave (p <= 2LS) or per half-wave, lane = hit
+        // index: a half-wave's hits lie in distinct columns, so a bank (two
+        // columns) sees at most two of them.
+        const uint32_t i = i_mid1 + k * 64 + lane;
+        const bool ok = i < i_big;
+        const uint32_t pl = ok ? P[i] : 0u;
+        uint32_t bl = SEG;
+        if (ok) {
+          const uint64_t g0 = ((uint64_t)pl * pl - 3) >> 1;
+          if (g0 < seg_end) {
+            if (g0 >= G) bl = (uint32_t)(g0 - G);
+            else { const uint32_t d = mod_barrett(G - g0, pl, M[i]); bl = d ? pl - d : 0; }
+          }
+        }
+        const uint32_t nj = min(64u, i_big - (i_mid1 + k * 64));
+        const bool two = __builtin_amdgcn_readlane(pl, 0) > 2 * LS;  // sorted: the whole batch > 2LS
+        if (!two) {
+          for (uint32_t j = 0; j < nj; ++j) {
+            const uint32_t p = __builtin_amdgcn_readlane(pl, j);
+            const uint32_t b0 = __builtin_amdgcn_readlane(bl, j);
+            const uint32_t b = b0 + lane * p;
+            const uint32_t o = b & (LS - 1);
+            if (b < SEG) lds_or(seg + ((o >> 5) << 6) + (b >> LOG_LS), 1u << (o & 31));
+          }
+        } else {
+          const uint32_t hl = lane & 31;
+          for (uint32_t j = 0; j < nj; j += 2) {
+            const uint32_t pa = __builtin_amdgcn_readlane(pl, j), ba = __builtin_amdgcn_readlane(bl, j);
+            const uint32_t jb = j + 1 < nj ? j + 1 : j;
+            const uint32_t pb = __builtin_amdgcn_readlane(pl, jb), bbv = __builtin_amdgcn_readlane(bl, jb);
+            const bool lo_half = lane < 32;
+            const uint32_t p = lo_half ? pa : pb;
+            const uint32_t b = (lo_half ? ba : (j + 1 < nj ? bbv : SEG)) + hl * p;
+            const uint32_t o = b & (LS - 1);
+            if (b < SEG) lds_or(seg + ((o >> 5) << 6) + (b >> LOG_LS), 1u << (o & 31));
           }
         }
       } else {
-        // 64 large primes per wave, one per lane, anywhere in the segment
-        const uint32_t base = i_mid1 + (u - nA - nB) * 64;
-        const uint32_t p0 = P[base];
-        if ((((uint64_t)p0 * p0 - 3) >> 1) >= seg_end) break;
-        const uint32_t i = base + lane;
-        uint32_t b = SEG, p = 1;
-        if (i < np) {
-          p = P[i];
+        if (!(phases & kPhaseLarge)) continue;
+        // 256 primes > 4LS, 4 per lane, scattered anywhere in the segment
+        const uint32_t base = i_big + (k - nC) * 256;
+        uint32_t pr[4], b[4];
+        uint64_t mr[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t i = base + r * 64 + lane;
+          pr[r] = i < np ? P[i] : 1u;
+          mr[r] = i < np ? M[i] : 0ull;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t p = pr[r];
           const uint64_t g0 = ((uint64_t)p * p - 3) >> 1;
-          if (g0 < seg_end) {
-            if (g0 >= G) {
-              b = (uint32_t)(g0 - G);
-            } else {
-              const uint32_t d = mod_barrett(G - g0, p, M[i]);
-              b = d ? p - d : 0;
-            }
+          uint32_t bb = SEG;
+          if (p > 1 && g0 < seg_end) {
+            if (g0 >= G) bb = (uint32_t)(g0 - G);
+            else { const uint32_t d = mod_barrett(G - g0, p, mr[r]); bb = d ? p - d : 0; }
           }
+          b[r] = bb;
         }
-        // hits per lane differ little between neighbouring primes: run the
-        // wave-wide minimum without exec-mask churn, then the remainder
-        const uint32_t trips = b < SEG ? div_small(SEG - 1 - b, p, 1.0f / (float)p) + 1 : 0;
-        const uint32_t n_min = wave_min_u32(trips);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const uint32_t p = pr[r];
+          uint32_t bb = b[r];
+          // hits per lane differ little between neighbouring primes: run the
+          // wave-wide minimum without exec-mask churn, then the remainder
+          const uint32_t trips = bb < SEG ? div_small(SEG - 1 - bb, p, 1.0f / (float)p) + 1 : 0;
+          const uint32_t n_min = wave_min_u32(trips);
 #pragma unroll 2
-        for (uint32_t k = 0; k < n_min; ++k) {
-          const uint32_t o = b & (LS - 1);
-          lds_or(seg + ((o >> 5) << 6) + (b >> LOG_LS), 1u << (o & 31));
-          b += p;
-        }
-        for (; b < SEG; b += p) {
-          const uint32_t o = b & (LS - 1);
-          lds_or(seg + ((o >> 5) << 6) + (b >> LOG_LS), 1u << (o & 31));
+          for (uint32_t h = 0; h < n_min; ++h) {
+            const uint32_t o = bb & (LS - 1);
+            lds_or(seg + ((o >> 5) << 6) + (bb >> LOG_LS), 1u << (o & 31));
+            bb += p;
+          }
+          for (; bb < SEG; bb += p) {
+            const uint32_t o = bb & (LS - 1);
+            lds_or(seg + ((o >> 5) << 6) + (bb >> LOG_LS), 1u << (o & 31));
+          }
         }
       }
     }
@@ -296,6 +397,7 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
         uint64_t hi = (uint64_t)src[128] | ((uint64_t)src[192] << 32);
 #pragma unroll
         for (int k = 0; k < kNumSmall; ++k) {
+          if (!(phases & kPhaseSmall)) break;
           const uint32_t q = kSmall[k];
           const uint32_t d64 = 64 % q;
           uint32_t t = res[k];
@@ -315,7 +417,7 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
           hi = pos + 64 >= nbits ? 0 : (nbits - pos - 64 >= 64 ? hi : hi & ((1ull << (nbits - pos - 64)) - 1));
         }
         my_count += (unsigned long long)(__popcll(lo) + __popcll(hi));
-        if (out) {
+        if (out && (phases & kPhaseStore)) {
           const uint64_t wi = pos >> 5;
           if (wi + 4 <= out_words) {
             *reinterpret_cast<uint4*>(out + wi) =
@@ -433,8 +535,12 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
   constexpr uint64_t SEG = 1ull << kLogSeg;
   const uint64_t nseg = (nbits + SEG - 1) / SEG;
   const uint64_t grid = nseg < (uint64_t)num_cus ? nseg : (uint64_t)num_cus;
+  static const uint32_t phases = [] {
+    const char* e = getenv("DSE_PHASES");  // profiling-only ablation knob
+    return e ? (uint32_t)strtoul(e, nullptr, 0) : kPhaseAll;
+  }();
   hipLaunchKernelGGL((sieve_segments_kernel<kLogSeg, kThreads>), dim3((uint32_t)grid), dim3(kThreads), 0,
-                     stream, table, g_start, nbits, out, count);
+                     stream, table, g_start, nbits, out, count, phases);
   return hipGetLastError();
 }
 
