@@ -121,6 +121,46 @@ __device__ __forceinline__ uint32_t div_small(uint32_t t, uint32_t p, float invp
   return q;
 }
 
+
+// 16 diagonal column steps of one lane's prime with compile-time hit counts:
+// NU unconditional marks and NX value-predicated ones (OR 0 into the lane's
+// own column when past the column end) per column; no inner-loop control.
+template <uint32_t LS, int NU, int NX>
+__device__ __forceinline__ void diag_walk(char* __restrict__ segb, uint32_t off, uint32_t p, uint32_t c4,
+                                          uint32_t O0, bool valid) {
+#pragma unroll 2
+  for (uint32_t t = 0; t < 16; ++t) {
+#pragma unroll
+    for (int h = 0; h < NU; ++h) {
+      lds_or(reinterpret_cast<uint32_t*>(segb + (((off >> 5) << 8) | c4)), 1u << (off & 31));
+      off += p;
+    }
+#pragma unroll
+    for (int h = 0; h < NX; ++h) {
+      const bool hit = off < LS;
+      const uint32_t o = hit ? off : 0u;
+      lds_or(reinterpret_cast<uint32_t*>(segb + (((o >> 5) << 8) | c4)), hit ? 1u << (o & 31) : 0u);
+      off = hit ? off + p : off;
+    }
+    off -= LS;
+    c4 = (c4 + 4) & 255;
+    off = (c4 == 0 && valid) ? O0 : off;  // wrapped from column 63 to column 0
+  }
+}
+
+template <uint32_t LS, int U>
+__device__ __forceinline__ void diag_dispatch(uint32_t n_u, uint32_t n_x, char* __restrict__ segb, uint32_t off,
+                                              uint32_t p, uint32_t c4, uint32_t O0, bool valid) {
+  if constexpr (U <= 15) {
+    if (n_u == U) {
+      if (n_x == 1) diag_walk<LS, U, 1>(segb, off, p, c4, O0, valid);
+      else diag_walk<LS, U, 2>(segb, off, p, c4, O0, valid);
+      return;
+    }
+    diag_dispatch<LS, U + 1>(n_u, n_x, segb, off, p, c4, O0, valid);
+  }
+}
+
 constexpr uint32_t kMaxMid = 1920;  // mid primes staged in LDS (odd primes 67..16384: 1882)
 
 template <int LOG_SEG, int NT>
@@ -272,21 +312,24 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
         const uint32_t n_x = (LS + pmin - 1) / pmin - n_u;
         uint32_t c4 = c0 << 2;  // byte offset of the current column
         if (!valid) off = 0x40000000u;  // no marks: every predicated OR is 0
-        for (uint32_t t = 0; t < 16; ++t) {
-#pragma unroll 2
-          for (uint32_t h = 0; h < n_u; ++h) {
-            lds_or(reinterpret_cast<uint32_t*>(segb + (((off >> 5) << 8) | c4)), 1u << (off & 31));
-            off += p;
+        if (n_u >= 1 && n_u <= 15 && n_x >= 1 && n_x <= 2) {
+          diag_dispatch<LS, 1>(n_u, n_x, segb, off, p, c4, O0, valid);
+        } else {
+          for (uint32_t t = 0; t < 16; ++t) {
+            for (uint32_t h = 0; h < n_u; ++h) {
+              lds_or(reinterpret_cast<uint32_t*>(segb + (((off >> 5) << 8) | c4)), 1u << (off & 31));
+              off += p;
+            }
+            for (uint32_t h = 0; h < n_x; ++h) {
+              const bool hit = off < LS;
+              const uint32_t o = hit ? off : 0u;
+              lds_or(reinterpret_cast<uint32_t*>(segb + (((o >> 5) << 8) | c4)), hit ? 1u << (o & 31) : 0u);
+              off = hit ? off + p : off;
+            }
+            off -= LS;
+            c4 = (c4 + 4) & 255;
+            off = (c4 == 0 && valid) ? O0 : off;  // wrapped from column 63 to column 0
           }
-          for (uint32_t h = 0; h < n_x; ++h) {
-            const bool hit = off < LS;
-            const uint32_t o = hit ? off : 0u;
-            lds_or(reinterpret_cast<uint32_t*>(segb + (((o >> 5) << 8) | c4)), hit ? 1u << (o & 31) : 0u);
-            off = hit ? off + p : off;
-          }
-          off -= LS;
-          c4 = (c4 + 4) & 255;
-          off = (c4 == 0 && valid) ? O0 : off;  // wrapped from column 63 to column 0
         }
       } else if (k < nC) {
         if (!(phases & kPhaseLarge)) continue;
