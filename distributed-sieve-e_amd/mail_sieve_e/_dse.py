@@ -68,6 +68,14 @@ def lib() -> ctypes.CDLL:
             raise ImportError(
                 f"libdse.so not built at {LIB_PATH}; run `make -C {CSRC}` "
                 "(the HIP extension is required, there is no CPU fallback)")
+        # torch (the device-memory/stream plumbing) ships its own copy of
+        # libamdhip64.so.7; load it first so libdse binds to that same HIP
+        # runtime instead of /opt/rocm's (two runtimes in one process cannot
+        # both open the GPU, and torch's stream handles must be understood).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             f = getattr(L, name)

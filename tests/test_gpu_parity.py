@@ -1,0 +1,183 @@
+"""Parity of the HIP path (libdse.so on an MI355X) with the oracle.
+
+Small sizes: bit-exact masks/counts/files against the oracle's faithful
+restatement of sieve.clj (golden fixtures in tests/golden/golden.json and
+live oracle calls). Full sizes (1e9..1e12): mask SHA-256 against golden
+fixtures, published pi(10^k), and size-independent properties (chunk masks
+concatenate to the P=1 mask; P does not change pi_ref + tail).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLDEN = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).view(np.uint8).tobytes()).hexdigest()
+
+
+def test_golden_sweep_bit_exact(ctx):
+    """120 seeded (N, P) cases (seed 0x5EED, N in [20, 1e7], P in 1..8)."""
+    for case in GOLDEN["sweep"]:
+        N, P = case["N"], case["P"]
+        for k in range(P):
+            m, c = ctx.sieve_chunk(N, P, k + 1)
+            assert c == case["counts"][k], (N, P, k + 1)
+            assert sha(m) == case["mask_sha256"][k], (N, P, k + 1)
+
+
+def test_live_oracle_random_chunks(ctx, oracle):
+    rng = np.random.default_rng(0x5EED + 1)
+    for _ in range(40):
+        N = int(rng.integers(20, 3_000_000))
+        P = int(rng.integers(1, 9))
+        cs, _ = oracle.spread_work(N, P)
+        if cs < 1:
+            continue
+        _, masks, counts, _ = oracle.sieve(N, P)
+        counts_all, pi_ref, pi_full = ctx.sieve_all(N, P)
+        assert [int(x) for x in counts_all] == [int(x) for x in counts]
+        assert pi_ref == oracle.pi_ref(counts)
+        for k in range(P):
+            assert np.array_equal(ctx.copy_chunk_mask(N, P, k + 1), masks[k]), (N, P, k)
+
+
+@pytest.mark.parametrize("g0,nb", [(0, 1), (0, 2), (0, 3), (0, 31), (0, 32), (0, 33), (0, 63), (0, 64),
+                                   (0, 65), (0, 127), (0, 128), (0, 129), (5, 7), (29, 70), (31, 1000),
+                                   (2**20 - 3, 7), (2**20 - 64, 2**20 + 128), (10**6, 3 * 2**20 + 17),
+                                   (123456789, 2**21 - 1), (49_999_999_000, 999)])
+def test_ragged_ranges(ctx, oracle, g0, nb):
+    """Unaligned starts/lengths, partial words and segments, the small-prime
+    self-bits near index 0, p^2 crossing segment boundaries."""
+    m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
+    m, c = ctx.sieve_odd_range(g0, nb)
+    assert c == c_ref
+    assert np.array_equal(m, m_ref)
+
+
+def test_random_ranges(ctx, oracle):
+    rng = np.random.default_rng(11)
+    for _ in range(25):
+        g0 = int(rng.integers(0, 5 * 10**10))
+        nb = int(rng.integers(1, 5 * 2**20))
+        m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
+        m, c = ctx.sieve_odd_range(g0, nb)
+        assert c == c_ref and np.array_equal(m, m_ref), (g0, nb)
+
+
+def test_files_byte_exact(ctx, tmp_path):
+    from mail_sieve_e import sieve as S
+    for f in GOLDEN["files"]:
+        N, P, k = f["N"], f["P"], f["my_num"]
+        ch = S.gen_table(S.spread_work(N, P)[k - 1])
+        S.sieve_e(k, k == 1, None, ch, None, ctx=ctx, path=str(tmp_path / f"primes{k}.txt"))
+        b = (tmp_path / f"primes{k}.txt").read_bytes()
+        assert (len(b), b.count(b"\n"), hashlib.sha256(b).hexdigest()) == (f["bytes"], f["lines"], f["sha256"])
+
+
+def test_1e9_mask_golden(ctx):
+    g = GOLDEN["big"]["1e9_P1"]
+    m, c = ctx.sieve_chunk(g["N"], 1, 1)
+    assert c + 1 == g["pi_ref"] == 50_847_534
+    assert sha(m) == g["mask_sha256"][0]
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_1e10_chunks_golden(ctx, P):
+    g = GOLDEN["big"][f"1e10_P{P}"]
+    counts, pi_ref, pi_full = ctx.sieve_all(10**10, P)
+    assert [int(x) for x in counts] == g["counts"]
+    assert pi_ref == pi_full == 455_052_511
+    for k in range(P):
+        assert sha(ctx.copy_chunk_mask(10**10, P, k + 1)) == g["mask_sha256"][k]
+
+
+def test_chunks_concatenate_to_single_chunk(ctx):
+    """Size-independent property: the P chunk masks, laid end to end, are the
+    first P*cs bits of the P=1 mask (N=1e10 with P=8: cs is not a multiple of 64)."""
+    N, P = 10**10, 8
+    full, _ = ctx.sieve_chunk(N, 1, 1)
+    bits_full = np.unpackbits(full.view(np.uint8), bitorder="little")
+    ctx.sieve_all(N, P)
+    cs = (N - 1) // 2 // P
+    for k in range(P):
+        mk = ctx.copy_chunk_mask(N, P, k + 1)
+        bk = np.unpackbits(mk.view(np.uint8), bitorder="little")
+        assert np.array_equal(bk[:cs], bits_full[k * cs:(k + 1) * cs])
+        assert not bk[cs:].any()  # tail bits of the last word are zero
+
+
+@pytest.mark.parametrize("P", [1, 2, 4, 8])
+def test_pi_1e11(ctx, P):
+    counts, pi_ref, pi_full = ctx.sieve_all(10**11, P)
+    assert pi_ref == pi_full == 4_118_054_813
+    assert int(np.sum(counts)) + 1 == pi_ref
+
+
+def test_pi_1e12_dropped_tail(ctx):
+    """SURVEY.md Gotcha 1: the reference's chunks lose 999999999989."""
+    counts, pi_ref, pi_full = ctx.sieve_all(10**12, 8)
+    assert pi_ref == 37_607_912_017
+    assert pi_full == 37_607_912_018
+
+
+def test_idempotent(ctx):
+    a = ctx.sieve_chunk(10**9, 3, 2)
+    b = ctx.sieve_chunk(10**9, 3, 2)
+    assert a[1] == b[1] and np.array_equal(a[0], b[0])
+
+
+def test_window_small(ctx, oracle):
+    for lo, hi in [(10**12, 10**12 + 10**7), (2, 100), (1, 2), (4, 4), (999_999_999_989, 10**12)]:
+        a = max(lo, 3) | 1
+        if hi < a:
+            assert ctx.sieve_window(lo, hi) == 0
+            continue
+        g0, nb = (a - 3) // 2, ((hi if hi & 1 else hi - 1) - a) // 2 + 1
+        assert ctx.sieve_window(lo, hi) == oracle.fast_sieve_range(g0, nb, want_mask=False)[1]
+
+
+def test_device_api_with_torch(ctx):
+    """The *_dev_async entry points on torch tensors == the host entry point."""
+    import torch
+    from mail_sieve_e import sieve as S
+    g0, nb = 10**9, 3 * 2**20 + 5
+    limit = S.base_limit_for_range(g0, nb)
+    table = torch.empty(S.base_table_bytes(limit), dtype=torch.uint8, device="cuda")
+    mask = torch.empty((nb + 63) // 64, dtype=torch.int64, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    sp = torch.cuda.current_stream().cuda_stream
+    ctx.base_primes_dev_async(limit, table.data_ptr(), table.numel(), sp)
+    ctx.sieve_range_dev_async(table.data_ptr(), g0, nb, mask.data_ptr(), cnt.data_ptr(), sp)
+    torch.cuda.synchronize()
+    m_ref, c_ref = ctx.sieve_odd_range(g0, nb)
+    assert int(cnt.item()) == c_ref
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), m_ref)
+
+
+def test_errors_fail_loudly(ctx):
+    from mail_sieve_e import _dse
+    with pytest.raises(_dse.DseError):
+        ctx.sieve_chunk(10**6, 3, 4)          # my_num outside 1..P
+    with pytest.raises(_dse.DseError):
+        ctx.sieve_window(10**18, 10**18 + 10**6)  # base primes beyond the device table (for now)
+
+
+def test_core_lead_single_machine_gpu(tmp_path, oracle):
+    """core.lead_start with the HIP engine (P=1: no follower), nccl process group."""
+    import socket
+    from mail_sieve_e import core
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    r = core.lead_start(1, 10**6, port, out_dir=str(tmp_path))
+    assert (r.my_num, r.count, r.pi_ref, r.pi_full) == (1, 78497, 78498, 78498)
+    _, masks, _, _ = oracle.sieve(10**6, 1)
+    oracle.finish(str(tmp_path / "ref.txt"), 1, 10**6, 1, masks[0])
+    assert (tmp_path / "primes1.txt").read_bytes() == (tmp_path / "ref.txt").read_bytes()
