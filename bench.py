@@ -28,7 +28,7 @@ from mail_sieve_e import sieve as S  # noqa: E402
 from mail_sieve_e import work  # noqa: E402
 
 METRIC = "sieved integers/sec at N=1e11, 1/2/4/8 MI355X; % of LDS/HBM roofline"
-KNOWN_PI = {10**9: 50847534, 10**10: 455052511, 10**11: 4118054813, 10**12: 37607912018}
+KNOWN_PI = {10**9: 50847534, 3 * 10**9: 144449537, 10**10: 455052511, 10**11: 4118054813, 10**12: 37607912018}
 
 
 def parse():
@@ -39,7 +39,7 @@ def parse():
     ap.add_argument("--n", type=float, default=1e11, help="sieve limit N (default 1e11, the headline)")
     ap.add_argument("--no-mask", action="store_true", help="count only (not the product path; diagnostics)")
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
-    ap.add_argument("--cpu-sample-n", type=float, default=1e9)
+    ap.add_argument("--cpu-sample-n", type=float, default=3e9)
     return ap.parse_args()
 
 
@@ -56,6 +56,28 @@ def cpu_baseline(sample_n: int) -> dict:
             "sample": f"N={sample_n:.0e}, P=1 chunk: oracle/dse_oracle.c ref_sieve (faithful C restatement of "
                       f"sieve.clj's per-prime lead loop, {msgs} prime messages), {dt:.2f} s on 1 host core; "
                       "the Clojure reference cannot run (no JVM in the image)"}
+
+
+def pmc_traffic(N: int, P: int):
+    """HBM bytes per sieve launch from the committed rocprofv3 PMC passes for
+    this config (profiles/<round>/pmc_{fetch,write}_sieve_kernel.csv, N=1e11,
+    P=1), with the gfx950 correction of MI355X_MICROARCH.md: FETCH_SIZE counts
+    half of a wide coalesced read, WRITE_SIZE is exact; both in KiB."""
+    import csv
+    import glob
+    if (N, P) != (10**11, 1):
+        return None, None
+    for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")), reverse=True):
+        try:
+            vals = {}
+            for f, name in (("pmc_fetch_sieve_kernel.csv", "FETCH_SIZE"), ("pmc_write_sieve_kernel.csv", "WRITE_SIZE")):
+                rows = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(d, f)))
+                        if r["Counter_Name"] == name]
+                vals[name] = sum(rows) / len(rows)
+            return (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024, os.path.relpath(d, ROOT)
+        except (OSError, KeyError, ZeroDivisionError):
+            continue
+    return None, None
 
 
 def main():
@@ -121,11 +143,10 @@ def main():
         dist.all_reduce(kern_t, op=dist.ReduceOp.MAX)
     c = counts.cpu().tolist()
     pi_ref, pi_full = 1 + c[0], 1 + c[0] + c[1]
-    if world == 1:
-        pass
     T = elapsed.item()
     if rank == 0:
         rf = work.roofline(g0, cs, kern_t.item())
+        traffic, traffic_src = pmc_traffic(N, P) if not a.no_mask else (None, None)
         out = {
             "metric": METRIC,
             "value": N * a.steps / T,
@@ -149,7 +170,8 @@ def main():
             "roofline": {"bound": rf["bound"],
                          "achieved": rf["lds_achieved_gbs"] if rf["bound"] == "lds" else rf["hbm_achieved_gbs"],
                          "peak": work.LDS_PEAK_GBS if rf["bound"] == "lds" else work.HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": rf["frac"], "traffic": None,
+                         "unit": "GB/s", "frac": rf["frac"], "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "sieve_segments_kernel<20,1024>", "kernel_ms": kern_t.item() * 1e3,
                          "marks_per_launch": rf["marks"], "bytes_per_mark": work.BYTES_PER_MARK,
                          "hbm_bytes_per_launch": rf["hbm_bytes"], "hbm_achieved": rf["hbm_achieved_gbs"],
