@@ -161,7 +161,9 @@ __device__ __forceinline__ void diag_dispatch(uint32_t n_u, uint32_t n_x, char* 
   }
 }
 
-constexpr uint32_t kMaxMid = 1920;  // mid primes staged in LDS (odd primes 67..16384: 1882)
+// mid primes staged in LDS: odd primes in (61, LS] (16384: 1882, 8192: 1009)
+template <uint32_t LS>
+constexpr uint32_t max_mid() { return LS >= 16384 ? 1920u : LS >= 8192 ? 1024u : 512u; }
 
 template <int LOG_SEG, int NT>
 __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restrict__ table,
@@ -179,6 +181,7 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
   static_assert(ROWS_PER_WAVE % 4 == 0, "write-back handles 4 rows per step");
 
   __shared__ __attribute__((aligned(16))) uint32_t seg[SEG / 32];
+  constexpr uint32_t kMaxMid = max_mid<LS>();
   __shared__ uint64_t s_mid_m[kMaxMid];
   __shared__ uint32_t s_mid_p[kMaxMid];
   __shared__ uint32_t s_ctr;
@@ -311,8 +314,10 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
         const uint32_t n_u = any_slow ? 0u : LS / pmax;
         const uint32_t n_x = (LS + pmin - 1) / pmin - n_u;
         uint32_t c4 = c0 << 2;  // byte offset of the current column
-        if (!valid) off = 0x40000000u;  // no marks: every predicated OR is 0
-        if (n_u >= 1 && n_u <= 15 && n_x >= 1 && n_x <= 2) {
+        // lanes past the batch end do no marks at all (their unconditional
+        // marks would address outside the segment)
+        if (!valid) {
+        } else if (n_u >= 1 && n_u <= 15 && n_x >= 1 && n_x <= 2) {
           diag_dispatch<LS, 1>(n_u, n_x, segb, off, p, c4, O0, valid);
         } else {
           for (uint32_t t = 0; t < 16; ++t) {
@@ -582,8 +587,20 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     const char* e = getenv("DSE_PHASES");  // profiling-only ablation knob
     return e ? (uint32_t)strtoul(e, nullptr, 0) : kPhaseAll;
   }();
-  hipLaunchKernelGGL((sieve_segments_kernel<kLogSeg, kThreads>), dim3((uint32_t)grid), dim3(kThreads), 0,
-                     stream, table, g_start, nbits, out, count, phases);
+  static const int cfg = [] {
+    const char* e = getenv("DSE_CFG");  // profiling-only: 0 = 2^20 x 1 WG/CU, 1 = 2^19 x 2 WG/CU
+    return e ? atoi(e) : 0;
+  }();
+  if (cfg == 1) {
+    constexpr uint64_t SEG1 = 1ull << 19;
+    const uint64_t nseg1 = (nbits + SEG1 - 1) / SEG1;
+    const uint64_t grid1 = nseg1 < 2ull * num_cus ? nseg1 : 2ull * num_cus;
+    hipLaunchKernelGGL((sieve_segments_kernel<19, 512>), dim3((uint32_t)grid1), dim3(512), 0, stream, table,
+                       g_start, nbits, out, count, phases);
+  } else {
+    hipLaunchKernelGGL((sieve_segments_kernel<kLogSeg, kThreads>), dim3((uint32_t)grid), dim3(kThreads), 0,
+                       stream, table, g_start, nbits, out, count, phases);
+  }
   return hipGetLastError();
 }
 
