@@ -24,6 +24,9 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "distributed-sieve-e_amd")]
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+from mail_sieve_e import _dse  # noqa: E402
+if os.environ.get("DSE_LIB"):  # profiling only: A/B another build of the library
+    _dse.LIB_PATH = os.environ["DSE_LIB"]
 from mail_sieve_e import sieve as S  # noqa: E402
 from mail_sieve_e import work  # noqa: E402
 

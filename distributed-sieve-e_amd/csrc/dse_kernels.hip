@@ -27,8 +27,9 @@
 namespace dse {
 namespace {
 
-constexpr uint32_t kPhaseMidA = 1, kPhaseMidB = 2, kPhaseLarge = 4, kPhaseSmall = 8, kPhaseStore = 16;
-constexpr uint32_t kPhaseAll = 31;
+constexpr uint32_t kPhaseMidA = 1, kPhaseMidB = 2, kPhaseLarge = 4, kPhaseSmall = 8, kPhaseStore = 16,
+                   kPhaseScatter = 32;
+constexpr uint32_t kPhaseAll = 63;
 
 constexpr int kNumSmall = 17;
 constexpr uint32_t kSmall[kNumSmall] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61};
@@ -60,6 +61,8 @@ __device__ __forceinline__ uint32_t mod_barrett(uint64_t x, uint32_t p, uint64_t
 }
 
 // t mod p for t/p < 2^16, t < 2^24, via a float reciprocal and one fix-up.
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }  // ~1 ulp; users correct
+
 __device__ __forceinline__ uint32_t mod_small(uint32_t t, uint32_t p, float invp) {
   uint32_t q = (uint32_t)((float)t * invp);
   int32_t r = (int32_t)(t - q * p);
@@ -68,9 +71,6 @@ __device__ __forceinline__ uint32_t mod_small(uint32_t t, uint32_t p, float invp
   return (uint32_t)r;
 }
 
-__device__ __forceinline__ uint32_t wave_uniform(uint32_t v) {
-  return __builtin_amdgcn_readfirstlane(v);
-}
 
 // Per-column marking of one mid prime (p <= LS) in the fast case (p^2 at or
 // before the segment): lane L = column L starts at the first multiple at or
@@ -106,11 +106,6 @@ __device__ __forceinline__ void mark_column_slow(uint32_t* __restrict__ col, uin
   for (; off < LS; off += p) lds_or(col + ((off >> 5) << 6), 1u << (off & 31));
 }
 
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
-  return wave_uniform(v);
-}
 
 // floor(t / p) for t < 2^24 via a float reciprocal, corrected.
 __device__ __forceinline__ uint32_t div_small(uint32_t t, uint32_t p, float invp) {
@@ -258,7 +253,7 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
     for (;;) {
       uint32_t u = 0;
       if (lane == 0) u = atomicAdd(&s_ctr, 1u);
-      u = wave_uniform(__shfl(u, 0));
+      u = __builtin_amdgcn_readlane(u, 0);
       if (u >= n_units) break;
       // map u -> (list, index)
       bool in_s1;
@@ -273,7 +268,7 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
         const uint64_t g0 = ((uint64_t)p * p - 3) >> 1;  // index of p^2
         if (g0 >= seg_end) continue;
         if (g0 <= G) {
-          const float invp = 1.0f / (float)p;
+          const float invp = fast_rcp((float)p);
           mark_column<LS>(col, lane, p, mod_barrett(G - g0, p, m), mod_small(LS, p, invp), invp);
         } else {
           mark_column_slow<LS>(col, lane, p, m, g0, G);
@@ -300,7 +295,7 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
             O0 = (uint32_t)(g0 - G);
           }
         }
-        const float invp = 1.0f / (float)p;
+        const float invp = fast_rcp((float)p);
         const uint32_t c0 = (lane + 16 * q) & 63;
         const uint32_t cstart = c0 * LS;
         uint32_t off;
@@ -311,8 +306,8 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
         const uint32_t pmin = __builtin_amdgcn_readlane(p, 0);
         const uint32_t pmax = __builtin_amdgcn_readlane(p, nj - 1);
         const bool any_slow = __builtin_amdgcn_ballot_w64(valid && O0 >= p) != 0;
-        const uint32_t n_u = any_slow ? 0u : LS / pmax;
-        const uint32_t n_x = (LS + pmin - 1) / pmin - n_u;
+        const uint32_t n_u = any_slow ? 0u : div_small(LS, pmax, fast_rcp((float)pmax));
+        const uint32_t n_x = div_small(LS + pmin - 1, pmin, fast_rcp((float)pmin)) - n_u;
         uint32_t c4 = c0 << 2;  // byte offset of the current column
         // lanes past the batch end do no marks at all (their unconditional
         // marks would address outside the segment)
@@ -377,7 +372,7 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
           }
         }
       } else {
-        if (!(phases & kPhaseLarge)) continue;
+        if (!(phases & kPhaseScatter)) continue;
         // 256 primes > 4LS, 4 per lane, scattered anywhere in the segment
         const uint32_t base = i_big + (k - nC) * 256;
         uint32_t pr[4], b[4];
@@ -405,8 +400,13 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
           uint32_t bb = b[r];
           // hits per lane differ little between neighbouring primes: run the
           // wave-wide minimum without exec-mask churn, then the remainder
-          const uint32_t trips = bb < SEG ? div_small(SEG - 1 - bb, p, 1.0f / (float)p) + 1 : 0;
-          const uint32_t n_min = wave_min_u32(trips);
+          // every lane with its first hit bb < p <= pmax has > (SEG-pmax)/pmax
+          // hits; any other lane (table end, p^2 inside or past the segment)
+          // forces the divergent loop. No cross-lane reduction: a ds_bpermute
+          // would wait for all of this wave's outstanding ds_or.
+          const uint32_t pmax = __builtin_amdgcn_readlane(p, 63);
+          const bool none = __builtin_amdgcn_ballot_w64(bb >= p) != 0;
+          const uint32_t n_min = none ? 0u : div_small(SEG - pmax, pmax, fast_rcp((float)pmax));
 #pragma unroll 2
           for (uint32_t h = 0; h < n_min; ++h) {
             const uint32_t o = bb & (LS - 1);

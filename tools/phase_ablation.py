@@ -3,8 +3,8 @@ process per variant is avoided by re-exec-free subprocess runs. Profiling only."
 import os, subprocess, sys, json
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N = sys.argv[1] if len(sys.argv) > 1 else "1e11"
-variants = {"all": 31, "no_store": 15, "no_small": 23, "no_large": 27, "no_midB": 29, "no_midA": 30,
-            "only_midA": 1 | 16, "only_midB": 2 | 16, "only_large": 4 | 16, "only_small": 8 | 16, "only_zero_wb": 16, "nothing": 0}
+variants = {"all": 63, "no_store": 47, "no_small": 55, "only_midA": 1 | 16, "only_midB": 2 | 16,
+            "only_coopC": 4 | 16, "only_scatterD": 32 | 16, "only_small": 8 | 16, "only_zero_wb": 16, "nothing": 0}
 for name, ph in variants.items():
     env = dict(os.environ, DSE_PHASES=str(ph))
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "2",
