@@ -111,12 +111,12 @@ int32_t ensure_counts(DevState& d, uint64_t n) {
 }
 
 int32_t build_table(DevState& d, uint64_t limit) {
-  if (limit > dse::kBaseLimitMax)
+  if (limit > dse::kBigBaseLimitMax)
     return fail(DSE_ERANGE, "base-prime limit " + std::to_string(limit) + " above the supported " +
-                                std::to_string(dse::kBaseLimitMax));
+                                std::to_string(dse::kBigBaseLimitMax));
   int32_t rc = ensure_table(d, limit);
   if (rc) return rc;
-  HIP_TRY(dse::launch_base_primes(limit, d.table, prime_cap(limit), d.stream));
+  HIP_TRY(dse::launch_base_primes_big(limit, d.table, prime_cap(limit), d.num_cus, d.stream));
   return DSE_OK;
 }
 
@@ -248,7 +248,7 @@ int32_t dse_tail_range(int64_t n, int32_t P, uint64_t* g_start, uint64_t* nbits)
 
 uint64_t dse_base_table_bytes(uint64_t limit) { return dse::table_bytes_for_cap(prime_cap(limit)); }
 
-uint64_t dse_base_limit_max(void) { return dse::kBaseLimitMax; }
+uint64_t dse_base_limit_max(void) { return dse::kBigBaseLimitMax; }
 
 uint64_t dse_base_limit_for_range(uint64_t g_start, uint64_t nbits) {
   if (nbits == 0) return 0;
@@ -260,9 +260,10 @@ int32_t dse_base_primes_dev_async(dse_ctx* ctx, uint64_t limit, void* table_dev,
                                   void* stream) {
   if (!ctx || !table_dev) return fail(DSE_EINVAL, "null ctx or table");
   if (table_bytes < dse_base_table_bytes(limit)) return fail(DSE_EINVAL, "table buffer too small");
-  if (limit > dse::kBaseLimitMax) return fail(DSE_ERANGE, "base-prime limit above the supported maximum");
+  if (limit > dse::kBigBaseLimitMax) return fail(DSE_ERANGE, "base-prime limit above the supported maximum");
   HIP_TRY(hipSetDevice(ctx->devs[0].device));
-  HIP_TRY(dse::launch_base_primes(limit, table_dev, prime_cap(limit), (hipStream_t)stream));
+  HIP_TRY(dse::launch_base_primes_big(limit, table_dev, prime_cap(limit), ctx->devs[0].num_cus,
+                                      (hipStream_t)stream));
   return DSE_OK;
 }
 
@@ -442,9 +443,9 @@ int32_t dse_sieve_window(dse_ctx* ctx, uint64_t lo, uint64_t hi, uint64_t* count
   const uint64_t b = (hi & 1) ? hi : hi - 1;
   const uint64_t g0 = (a - 3) / 2, nb = (b - a) / 2 + 1;
   const uint64_t limit = dse_base_limit_for_range(g0, nb);
-  if (limit > dse::kBaseLimitMax)
+  if (limit > dse::kBigBaseLimitMax)
     return fail(DSE_ERANGE, "window needs base primes up to " + std::to_string(limit) +
-                                "; the device base-prime kernel supports " + std::to_string(dse::kBaseLimitMax));
+                                "; the device base-prime build supports " + std::to_string(dse::kBigBaseLimitMax));
   const int nd = (int)ctx->devs.size();
   int32_t rc;
   for (int i = 0; i < nd; ++i) {

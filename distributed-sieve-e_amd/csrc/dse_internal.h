@@ -31,7 +31,13 @@ constexpr int kSmallMax = 61;             // primes <= 61: register patterns at 
 // Largest limit the single-workgroup base-prime kernel handles (LDS bitmap).
 constexpr uint64_t kBaseLimitMax = 2ull * 150u * 1024u * 8u + 1ull;  // 150 KiB of odd bits
 
+// Big tables: odd primes < 2^31 (so p + SEG fits 32 bits in the kernel).
+constexpr uint64_t kBigBaseLimitMax = (1ull << 31) - 1;
+
 hipError_t launch_base_primes(uint64_t limit, void* table, uint32_t cap, hipStream_t stream);
+// Any limit <= kBigBaseLimitMax: the one-workgroup kernel up to kBaseLimitMax,
+// above it a sieve of [3, limit] by the segment kernel + ordered compaction.
+hipError_t launch_base_primes_big(uint64_t limit, void* table, uint32_t cap, int num_cus, hipStream_t stream);
 
 // Sieve odd indices [g_start, g_start+nbits): out (may be null) gets the mask as
 // 32-bit words (2*ceil(nbits/64) of them, upper half of the last uint64 zeroed);

@@ -406,7 +406,8 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
           // would wait for all of this wave's outstanding ds_or.
           const uint32_t pmax = __builtin_amdgcn_readlane(p, 63);
           const bool none = __builtin_amdgcn_ballot_w64(bb >= p) != 0;
-          const uint32_t n_min = none ? 0u : div_small(SEG - pmax, pmax, fast_rcp((float)pmax));
+          // (primes above SEG hit a segment at most once: divergent loop only)
+          const uint32_t n_min = (none || pmax > SEG) ? 0u : div_small(SEG - pmax, pmax, fast_rcp((float)pmax));
 #pragma unroll 2
           for (uint32_t h = 0; h < n_min; ++h) {
             const uint32_t o = bb & (LS - 1);
@@ -568,12 +569,155 @@ __global__ __launch_bounds__(1024) void base_primes_kernel(uint64_t limit, void*
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Big base-prime tables (limit above kBaseLimitMax, e.g. 1e9 for the 1e18
+// window): sieve [3, limit] with the segment kernel itself, then compact the
+// prime bits into an ordered table. Scratch lives in the table's m[] region,
+// which is only written at the very end.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kCompactWordsPerThread = 8;
+constexpr uint32_t kCompactThreads = 256;
+constexpr uint32_t kCompactBlockWords = kCompactWordsPerThread * kCompactThreads;  // 2048 words
+
+__global__ __launch_bounds__(kCompactThreads) void compact_count_kernel(const uint64_t* __restrict__ mask,
+                                                                        uint64_t words,
+                                                                        uint32_t* __restrict__ block_sums) {
+  __shared__ uint32_t s_part[kCompactThreads / 64];
+  const uint64_t w0 = (uint64_t)blockIdx.x * kCompactBlockWords + threadIdx.x * kCompactWordsPerThread;
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kCompactWordsPerThread; ++k)
+    if (w0 + k < words) c += __popcll(mask[w0 + k]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < kCompactThreads / 64; ++w) t += s_part[w];
+    block_sums[blockIdx.x] = t;
+  }
+}
+
+// exclusive scan of block sums in place; total -> table header count
+__global__ __launch_bounds__(1024) void compact_scan_kernel(uint32_t* __restrict__ block_sums, uint32_t nblocks,
+                                                            void* __restrict__ table, uint32_t cap, uint64_t limit) {
+  __shared__ uint32_t s_scan[1024];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t per = (nblocks + 1023) / 1024;
+  const uint32_t b0 = tid * per, b1 = min(nblocks, b0 + per);
+  uint32_t sum = 0;
+  for (uint32_t b = b0; b < b1; ++b) sum += block_sums[b];
+  s_scan[tid] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {
+    const uint32_t x = tid >= o ? s_scan[tid - o] : 0;
+    __syncthreads();
+    s_scan[tid] += x;
+    __syncthreads();
+  }
+  uint32_t run = s_scan[tid] - sum;
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t v = block_sums[b];
+    block_sums[b] = run;
+    run += v;
+  }
+  if (tid == 1023) {
+    TableHeader* h = reinterpret_cast<TableHeader*>(table);
+    const uint32_t total = s_scan[1023];
+    h->count = total <= cap ? total : 0xFFFFFFFFu;
+    h->cap = cap;
+    h->limit = limit;
+  }
+}
+
+__global__ __launch_bounds__(kCompactThreads) void compact_write_kernel(const uint64_t* __restrict__ mask,
+                                                                        uint64_t words,
+                                                                        const uint32_t* __restrict__ block_offs,
+                                                                        uint32_t* __restrict__ P, uint32_t cap) {
+  __shared__ uint32_t s_scan[kCompactThreads];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t w0 = (uint64_t)blockIdx.x * kCompactBlockWords + tid * kCompactWordsPerThread;
+  uint64_t v[kCompactWordsPerThread];
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kCompactWordsPerThread; ++k) {
+    v[k] = w0 + k < words ? mask[w0 + k] : 0ull;
+    c += __popcll(v[k]);
+  }
+  s_scan[tid] = c;
+  __syncthreads();
+  for (uint32_t o = 1; o < kCompactThreads; o <<= 1) {
+    const uint32_t x = tid >= o ? s_scan[tid - o] : 0;
+    __syncthreads();
+    s_scan[tid] += x;
+    __syncthreads();
+  }
+  uint32_t pos = block_offs[blockIdx.x] + s_scan[tid] - c;
+#pragma unroll
+  for (uint32_t k = 0; k < kCompactWordsPerThread; ++k) {
+    uint64_t x = v[k];
+    while (x) {
+      const uint32_t b = __ffsll((long long)x) - 1;
+      x &= x - 1;
+      if (pos < cap) P[pos] = (uint32_t)(3 + 2 * ((w0 + k) * 64 + b));
+      ++pos;
+    }
+  }
+}
+
+__global__ void barrett_kernel(const void* __restrict__ table, uint64_t* __restrict__ M) {
+  const TableHeader* h = reinterpret_cast<const TableHeader*>(table);
+  const uint32_t n = h->count == 0xFFFFFFFFu ? 0u : h->count;
+  const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    M[i] = ~0ull / P[i];
+}
+
 }  // namespace
 
 hipError_t launch_base_primes(uint64_t limit, void* table, uint32_t cap, hipStream_t stream) {
   if (limit > kBaseLimitMax) return hipErrorInvalidValue;
   if (limit > 2ull * 32ull * kBaseWords + 1ull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(base_primes_kernel, dim3(1), dim3(1024), 0, stream, limit, table, cap);
+  return hipGetLastError();
+}
+
+
+hipError_t launch_base_primes_big(uint64_t limit, void* table, uint32_t cap, int num_cus, hipStream_t stream) {
+  if (limit <= kBaseLimitMax) return launch_base_primes(limit, table, cap, stream);
+  if (limit > kBigBaseLimitMax) return hipErrorInvalidValue;
+  // scratch carved from the m[] region: [mask][level-0 table][block sums][count]
+  char* mreg = reinterpret_cast<char*>(table) + table_m_offset(cap);
+  const uint64_t nb = (limit - 3) / 2 + 1;            // odd values 3..limit
+  const uint64_t words = (nb + 63) / 64;
+  uint64_t* mask = reinterpret_cast<uint64_t*>(mreg);
+  const uint64_t lim0 = [&] {                          // isqrt(limit)
+    uint64_t r = (uint64_t)__builtin_sqrt((double)limit);
+    while (r * r > limit) --r;
+    while ((r + 1) * (r + 1) <= limit) ++r;
+    return r;
+  }();
+  const uint32_t cap0 = (uint32_t)(1.26 * (double)lim0 / __builtin_log((double)(lim0 > 100 ? lim0 : 100))) + 64;
+  char* t0 = mreg + ((words * 8 + 255) & ~255ull);
+  const uint64_t t0_bytes = (table_bytes_for_cap(cap0) + 255) & ~255ull;
+  const uint32_t nblocks = (uint32_t)((words + kCompactBlockWords - 1) / kCompactBlockWords);
+  uint32_t* sums = reinterpret_cast<uint32_t*>(t0 + t0_bytes);
+  unsigned long long* cnt = reinterpret_cast<unsigned long long*>(sums + ((nblocks + 63) & ~63u));
+  if ((uint64_t)(reinterpret_cast<char*>(cnt + 1) - mreg) > 8ull * cap) return hipErrorInvalidValue;
+  hipError_t e = launch_base_primes(lim0, t0, cap0, stream);
+  if (e != hipSuccess) return e;
+  if ((e = hipMemsetAsync(cnt, 0, sizeof(*cnt), stream)) != hipSuccess) return e;
+  if ((e = launch_sieve_range(t0, 0, nb, reinterpret_cast<uint32_t*>(mask), cnt, num_cus, stream)) != hipSuccess)
+    return e;
+  hipLaunchKernelGGL(compact_count_kernel, dim3(nblocks), dim3(kCompactThreads), 0, stream, mask, words, sums);
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, stream, sums, nblocks, table, cap, limit);
+  uint32_t* P = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + 16);
+  hipLaunchKernelGGL(compact_write_kernel, dim3(nblocks), dim3(kCompactThreads), 0, stream, mask, words, sums, P,
+                     cap);
+  hipLaunchKernelGGL(barrett_kernel, dim3(4 * (uint32_t)num_cus), dim3(256), 0, stream, table,
+                     reinterpret_cast<uint64_t*>(mreg));
   return hipGetLastError();
 }
 
