@@ -10,6 +10,8 @@ namespace dse {
 //   [0,16)            header {count, cap, limit}
 //   [16, 16+4cap)     uint32 p[cap]      odd primes <= limit, ascending
 //   [align8(...), +8cap) uint64 m[cap]  Barrett factors floor((2^64-1)/p)
+//   [.., +32cap)      uint32 a[8cap]     wheel offsets: a[8i+j] = first k >= 0 with
+//                                        p | R30[j] + 30k (p >= 7; 0 for p = 3, 5)
 struct TableHeader {
   uint32_t count;
   uint32_t cap;
@@ -19,9 +21,21 @@ struct TableHeader {
 __host__ __device__ inline uint64_t table_m_offset(uint32_t cap) {
   return (16ull + 4ull * cap + 7ull) & ~7ull;
 }
+__host__ __device__ inline uint64_t table_a_offset(uint32_t cap) { return table_m_offset(cap) + 8ull * cap; }
 __host__ __device__ inline uint64_t table_bytes_for_cap(uint32_t cap) {
-  return table_m_offset(cap) + 8ull * cap;
+  return table_a_offset(cap) + 32ull * cap;
 }
+
+// The 8 residues mod 30 coprime to 30 (wheel planes, absolute numbering).
+constexpr uint32_t kR30[8] = {1, 7, 11, 13, 17, 19, 23, 29};
+
+// Mod-30 wheel segment geometry (dse_wheel.hip): 2^17 periods of 30 integers,
+// 8 planes (one per coprime residue) x 8 columns of 2^14 periods each.
+constexpr int kWheelLogKP = 17;
+constexpr uint64_t kWheelSpan = 30ull << kWheelLogKP;   // integers per segment
+constexpr uint64_t kWheelOutBits = kWheelSpan / 2;      // odd candidates per segment
+// Largest base prime the wheel kernel takes (above: odd-only kernel for now).
+constexpr uint64_t kWheelMaxPrime = 1ull << 21;
 
 // Segment geometry of the marking kernel (see DESIGN.md "Kernels").
 constexpr int kLogSeg = 20;               // 2^20 odd candidates per LDS segment (128 KiB)
@@ -44,5 +58,14 @@ hipError_t launch_base_primes_big(uint64_t limit, void* table, uint32_t cap, int
 // *count (device) is incremented.
 hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
                               unsigned long long* count, int num_cus, hipStream_t stream);
+
+// The two marking kernels behind launch_sieve_range: the odd-only kernel
+// (dse_kernels.hip) and the mod-30 wheel kernel (dse_wheel.hip).
+hipError_t launch_sieve_range_odd(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
+                                  unsigned long long* count, int num_cus, hipStream_t stream);
+hipError_t launch_sieve_range_wheel(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
+                                    unsigned long long* count, int num_cus, hipStream_t stream);
+// Fill the wheel offsets a[] of a table whose p[] and m[] are final.
+hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream);
 
 }  // namespace dse

@@ -681,7 +681,9 @@ hipError_t launch_base_primes(uint64_t limit, void* table, uint32_t cap, hipStre
   if (limit > kBaseLimitMax) return hipErrorInvalidValue;
   if (limit > 2ull * 32ull * kBaseWords + 1ull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(base_primes_kernel, dim3(1), dim3(1024), 0, stream, limit, table, cap);
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_wheel_offsets(table, 64, stream);
 }
 
 
@@ -705,7 +707,7 @@ hipError_t launch_base_primes_big(uint64_t limit, void* table, uint32_t cap, int
   const uint32_t nblocks = (uint32_t)((words + kCompactBlockWords - 1) / kCompactBlockWords);
   uint32_t* sums = reinterpret_cast<uint32_t*>(t0 + t0_bytes);
   unsigned long long* cnt = reinterpret_cast<unsigned long long*>(sums + ((nblocks + 63) & ~63u));
-  if ((uint64_t)(reinterpret_cast<char*>(cnt + 1) - mreg) > 8ull * cap) return hipErrorInvalidValue;
+  if ((uint64_t)(reinterpret_cast<char*>(cnt + 1) - mreg) > 40ull * cap) return hipErrorInvalidValue;
   hipError_t e = launch_base_primes(lim0, t0, cap0, stream);
   if (e != hipSuccess) return e;
   if ((e = hipMemsetAsync(cnt, 0, sizeof(*cnt), stream)) != hipSuccess) return e;
@@ -718,11 +720,12 @@ hipError_t launch_base_primes_big(uint64_t limit, void* table, uint32_t cap, int
                      cap);
   hipLaunchKernelGGL(barrett_kernel, dim3(4 * (uint32_t)num_cus), dim3(256), 0, stream, table,
                      reinterpret_cast<uint64_t*>(mreg));
-  return hipGetLastError();
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return launch_wheel_offsets(table, num_cus, stream);
 }
 
-hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
-                              unsigned long long* count, int num_cus, hipStream_t stream) {
+hipError_t launch_sieve_range_odd(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
+                                  unsigned long long* count, int num_cus, hipStream_t stream) {
   if (nbits == 0) return hipSuccess;
   constexpr uint64_t SEG = 1ull << kLogSeg;
   const uint64_t nseg = (nbits + SEG - 1) / SEG;
