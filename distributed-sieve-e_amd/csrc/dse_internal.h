@@ -10,8 +10,9 @@ namespace dse {
 //   [0,16)            header {count, cap, limit}
 //   [16, 16+4cap)     uint32 p[cap]      odd primes <= limit, ascending
 //   [align8(...), +8cap) uint64 m[cap]  Barrett factors floor((2^64-1)/p)
-//   [.., +32cap)      uint32 a[8cap]     wheel offsets: a[8i+j] = first k >= 0 with
-//                                        p | R30[j] + 30k (p >= 7; 0 for p = 3, 5)
+//   [align32(..), +32cap) uint32 a[8cap] wheel offsets, row i rotated by i mod 8:
+//                                        a[8i+j] = first k >= 0 with p | R30[(j+i)&7] + 30k
+//                                        (p >= 7; 0 for p = 3, 5)
 struct TableHeader {
   uint32_t count;
   uint32_t cap;
@@ -21,7 +22,9 @@ struct TableHeader {
 __host__ __device__ inline uint64_t table_m_offset(uint32_t cap) {
   return (16ull + 4ull * cap + 7ull) & ~7ull;
 }
-__host__ __device__ inline uint64_t table_a_offset(uint32_t cap) { return table_m_offset(cap) + 8ull * cap; }
+__host__ __device__ inline uint64_t table_a_offset(uint32_t cap) {
+  return (table_m_offset(cap) + 8ull * cap + 31ull) & ~31ull;
+}
 __host__ __device__ inline uint64_t table_bytes_for_cap(uint32_t cap) {
   return table_a_offset(cap) + 32ull * cap;
 }

@@ -702,7 +702,7 @@ hipError_t launch_base_primes_big(uint64_t limit, void* table, uint32_t cap, int
     return r;
   }();
   const uint32_t cap0 = (uint32_t)(1.26 * (double)lim0 / __builtin_log((double)(lim0 > 100 ? lim0 : 100))) + 64;
-  char* t0 = mreg + ((words * 8 + 255) & ~255ull);
+  char* t0 = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(mreg) + words * 8 + 255) & ~(uintptr_t)255);
   const uint64_t t0_bytes = (table_bytes_for_cap(cap0) + 255) & ~255ull;
   const uint32_t nblocks = (uint32_t)((words + kCompactBlockWords - 1) / kCompactBlockWords);
   uint32_t* sums = reinterpret_cast<uint32_t*>(t0 + t0_bytes);

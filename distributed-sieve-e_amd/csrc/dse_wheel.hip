@@ -42,8 +42,9 @@
 namespace dse {
 namespace {
 
-constexpr uint32_t kPhaseMidA = 1, kPhaseMidB = 2, kPhaseLarge = 4, kPhaseSmall = 8, kPhaseStore = 16;
-constexpr uint32_t kPhaseAll = 31;
+constexpr uint32_t kPhaseMidA = 1, kPhaseMidB = 2, kPhaseLarge = 4, kPhaseSmall = 8, kPhaseStore = 16,
+                   kPhaseExpand = 32, kPhaseUnits = 64;
+constexpr uint32_t kPhaseAll = 127;
 
 constexpr uint32_t KP = 1u << kWheelLogKP;  // periods per segment (per plane)
 constexpr uint32_t LOG_LS = 14;
@@ -75,8 +76,8 @@ struct WheelArgs {
   uint64_t nbits;      // odd candidates in the range
   uint64_t KB0;        // floor(V0 / 30)
   uint64_t rho_pack;   // rho_i in bits [5i, 5i+5)
-  uint32_t iota_pack;  // absolute residue index of plane i in bits [3i, 3i+3)
-  uint32_t e_bits;     // bit i: floor((V0 + rho_i)/30) = KB0 + 1
+  uint32_t pl_pack;    // plane of absolute residue R30[j] in bits [3j, 3j+3)
+  uint32_t e_iota;     // bit j: floor((V0 + rho)/30) = KB0 + 1 for the plane of R30[j]
   uint32_t fix0;       // output word 0 bits of the primes 3..61 inside the range
   uint32_t phases;
   uint8_t v0q[kNQ];    // V0 mod q
@@ -85,6 +86,30 @@ struct WheelArgs {
 __device__ __forceinline__ void lds_or(uint32_t* a, uint32_t v) {
   __hip_atomic_fetch_or(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+
+// 32-bit LDS byte address of a __shared__ pointer.
+__device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)p;
+}
+
+// Mark period `off` of the column whose word 0 is at LDS byte address `cb`:
+// the segment is 256-byte aligned and a column's byte offset is < 256, so the
+// row offset (off >> 5) * 256 and the column combine with one v_and_or (the
+// compiler emits and + add). Issued as asm: callers drain lgkmcnt before a
+// barrier (lds_drain), since the compiler's waitcnt pass does not see it.
+__device__ __forceinline__ void mark_col(uint32_t cb, uint32_t off) {
+  uint32_t a, b;
+  asm volatile(
+      "v_lshlrev_b32 %0, 3, %2\n\t"
+      "v_and_or_b32 %0, %0, %4, %3\n\t"
+      "v_lshlrev_b32 %1, %2, 1\n\t"
+      "ds_or_b32 %0, %1"
+      : "=&v"(a), "=&v"(b)
+      : "v"(off), "v"(cb), "s"(0xffffff00u)
+      : "memory");
+}
+
+__device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // x mod p for x < 2^63 with m = floor((2^64-1)/p).
 __host__ __device__ __forceinline__ uint32_t mod_barrett(uint64_t x, uint32_t p, uint64_t m) {
@@ -100,6 +125,13 @@ __host__ __device__ __forceinline__ uint32_t mod_barrett(uint64_t x, uint32_t p,
 }
 
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
+// Keeps a marking offset opaque to loop strength reduction, which otherwise
+// splits it into several induction variables (7 VALU per mark instead of 4).
+__device__ __forceinline__ uint32_t opaque(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
 
 // t mod p, t < 2^24
 __device__ __forceinline__ uint32_t mod_small(uint32_t t, uint32_t p, float invp) {
@@ -177,10 +209,11 @@ __device__ __forceinline__ void diag_walk(uint32_t* __restrict__ seg, uint32_t o
 #pragma unroll 2
   for (uint32_t t = 0; t < 8; ++t) {
     uint32_t* colp = seg + cb + c;
+    const uint32_t cb_col = lds_addr(seg) + 4 * (cb + c);
 #pragma unroll
     for (int h = 0; h < NU; ++h) {
-      lds_or(colp + ((off >> 5) << 6), 1u << (off & 31));
-      off += p;
+      mark_col(cb_col, off);
+      off = opaque(off + p);
     }
 #pragma unroll
     for (int h = 0; h < NX; ++h) {
@@ -220,16 +253,197 @@ __device__ __forceinline__ uint64_t transpose8(uint64_t x) {
   return x;
 }
 
+// v_perm_b32: byte n of the result = byte sel[n] of {hi:lo} (0-3 lo, 4-7 hi).
+__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
+  return __builtin_amdgcn_perm(hi, lo, sel);
+}
+
+// 4x4 byte transpose: T[q] byte i = P[i] byte q.
+__device__ __forceinline__ void byte_transpose4(const uint32_t* P, uint32_t* T) {
+  const uint32_t u0 = perm(P[1], P[0], 0x06020400u), u1 = perm(P[1], P[0], 0x07030501u);
+  const uint32_t v0 = perm(P[3], P[2], 0x06020400u), v1 = perm(P[3], P[2], 0x07030501u);
+  T[0] = perm(v0, u0, 0x05040100u);
+  T[2] = perm(v0, u0, 0x07060302u);
+  T[1] = perm(v1, u1, 0x05040100u);
+  T[3] = perm(v1, u1, 0x07060302u);
+}
+
+// ---- work units of the mark phase ----------------------------------------
+
+// A: one mid prime (61 < p <= TA) per wave; lane L walks column L =
+// (plane L>>3, column L&7).
+__device__ __forceinline__ void unit_A(uint32_t* __restrict__ seg, uint32_t pi, uint64_t m, uint64_t Vs,
+                                       uint64_t rho_pack, uint32_t lane) {
+  const uint32_t p = pi & 0xFFFFu, inv30 = pi >> 16;  // wave-uniform
+  const uint64_t p2 = (uint64_t)p * p;
+  const uint32_t Xs = mod_barrett(Vs, p, m);            // scalar unit
+  const float invp = fast_rcp((float)p);
+  const uint32_t pl = lane >> 3, c = lane & 7;
+  const uint32_t rho = (uint32_t)(rho_pack >> (5 * pl)) & 31u;
+  const uint32_t kp = plane_first(Xs, rho, p, inv30, invp);
+  const uint32_t cb_col = lds_addr(seg) + 4 * lane;
+  if (p2 <= Vs) {
+    const uint32_t cm = mod_small(c * LS, p, invp);
+    uint32_t off = kp >= cm ? kp - cm : kp + p - cm;
+    const uint32_t n_full = div_small(LS, p, invp);
+#pragma unroll 4
+    for (uint32_t h = 0; h < n_full; ++h) {
+      mark_col(cb_col, off);
+      off = opaque(off + p);
+    }
+    if (off < LS) mark_col(cb_col, off);
+  } else {
+    const uint32_t kmin = kmin_for((uint32_t)(p2 - Vs), rho);
+    const uint32_t kf = first_at_or_after(kp, max(kmin, c * LS), p, invp);
+    for (uint32_t off = kf - c * LS; off < LS; off += p) mark_col(cb_col, off);
+  }
+}
+
+// B: 8 mid primes (TA < p <= LS) x 8 planes; half-wave g takes planes
+// 4g..4g+3, lane (prime jp, plane pl) walks columns jp, jp+1, ... (mod 8):
+// at every step a half-wave is in 32 distinct columns.
+__device__ __forceinline__ void unit_B(uint32_t* __restrict__ seg, const uint32_t* __restrict__ s_mid_p,
+                                       const uint64_t* __restrict__ s_mid_m, uint32_t j0, uint32_t nj, uint64_t Vs,
+                                       uint64_t Vend, uint64_t rho_pack, uint32_t lane) {
+  const uint32_t pfirst = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
+  const uint32_t l = lane & 31;
+  const uint32_t pl = 4 * (lane >> 5) + (l & 3), jp = l >> 2;
+  const bool valid = jp < nj;
+  const uint32_t pi = s_mid_p[valid ? j0 + jp : j0];
+  const uint32_t p = pi & 0xFFFFu, inv30 = pi >> 16;
+  const uint64_t m = s_mid_m[valid ? j0 + jp : j0];
+  const float invp = fast_rcp((float)p);
+  const uint32_t rho = (uint32_t)(rho_pack >> (5 * pl)) & 31u;
+  const uint32_t Xs = mod_barrett(Vs, p, m);
+  const uint32_t kp = plane_first(Xs, rho, p, inv30, invp);
+  const uint64_t p2 = (uint64_t)p * p;
+  uint32_t O0, off;
+  const uint32_t cstart = jp * LS;
+  const bool slow = p2 > Vs;
+  if (!slow) {
+    O0 = kp;
+    const uint32_t cm = mod_small(cstart, p, invp);
+    off = kp >= cm ? kp - cm : kp + p - cm;
+  } else {
+    const uint32_t kmin = p2 >= Vend ? KP : kmin_for((uint32_t)(p2 - Vs), rho);
+    O0 = first_at_or_after(kp, kmin, p, invp);
+    off = first_at_or_after(kp, max(kmin, cstart), p, invp) - cstart;
+  }
+  const uint32_t pmin = pfirst;
+  const uint32_t pmax = __builtin_amdgcn_readfirstlane(s_mid_p[j0 + nj - 1]) & 0xFFFFu;
+  const bool any_slow = __builtin_amdgcn_ballot_w64(slow) != 0;
+  const uint32_t n_u = any_slow ? 0u : div_small(LS, pmax, fast_rcp((float)pmax));
+  const uint32_t n_x = div_ceil_small(LS, pmin, fast_rcp((float)pmin)) - n_u;
+  const uint32_t cb = 8 * pl;
+  // lanes past the batch end mark nothing (their unconditional marks would
+  // land in another prime's columns)
+  if (!valid) return;
+  if (n_u >= 1 && n_u <= 15 && n_x >= 1 && n_x <= 2) {
+    diag_dispatch<1>(n_u, n_x, seg, off, p, cb, jp, O0);
+    return;
+  }
+  uint32_t c = jp;
+  for (uint32_t t = 0; t < 8; ++t) {
+    uint32_t* colp = seg + cb + c;
+    const uint32_t cb_col = lds_addr(seg) + 4 * (cb + c);
+    for (uint32_t h = 0; h < n_u; ++h) {
+      mark_col(cb_col, off);
+      off += p;
+    }
+    for (uint32_t h = 0; h < n_x; ++h) {
+      const bool hit = off < LS;
+      const uint32_t o = hit ? off : 0u;
+      lds_or(colp + ((o >> 5) << 6), hit ? 1u << (o & 31) : 0u);
+      off = hit ? off + p : off;
+    }
+    off -= LS;
+    c = (c + 1) & 7;
+    off = c == 0 ? O0 : off;
+  }
+}
+
+// Operands of one large unit, loaded ahead of use. The table row of prime i
+// holds its 8 wheel offsets rotated by i mod 8, so lane L (i = 64u + L) reads
+// a[(q + L) & 7] at position q with two aligned 16-byte loads.
+struct LargeOps {
+  uint32_t p;
+  uint64_t m;
+  uint32_t a[8];
+};
+
+__device__ __forceinline__ void load_L(LargeOps& o, const uint32_t* __restrict__ P, const uint64_t* __restrict__ M,
+                                       const uint32_t* __restrict__ A, uint32_t il, uint32_t np) {
+  const bool ok = il < np;
+  o.p = ok ? P[il] : 0x7FFFFFFFu;
+  o.m = ok ? M[il] : 1ull;
+  const uint4* row = reinterpret_cast<const uint4*>(A + 8ull * il);
+  const uint4 lo = ok ? row[0] : make_uint4(0, 0, 0, 0), hi = ok ? row[1] : make_uint4(0, 0, 0, 0);
+  o.a[0] = lo.x; o.a[1] = lo.y; o.a[2] = lo.z; o.a[3] = lo.w;
+  o.a[4] = hi.x; o.a[5] = hi.y; o.a[6] = hi.z; o.a[7] = hi.w;
+}
+
+// L: 64 large primes (p > LS), one per lane; at step q lane L handles the
+// absolute residue (q + L) & 7, so a half-wave spreads over all 8 planes.
+__device__ __forceinline__ void unit_L(uint32_t* __restrict__ seg, const LargeOps& o, uint64_t Vs, uint64_t Vend,
+                                       uint64_t Kb, uint32_t pl_rot, uint32_t e_rot, uint64_t rho_pack) {
+  const uint32_t p = o.p;
+  const uint64_t p2 = (uint64_t)p * p;
+  const bool live = p2 < Vend;
+  const bool slow = p2 > Vs;
+  const uint32_t Kbm = mod_barrett(Kb, p, o.m);
+  const float invp = fast_rcp((float)p);
+  const uint32_t pmax = __builtin_amdgcn_readlane(p, 63);
+  const bool none = __builtin_amdgcn_ballot_w64(!live || slow) != 0;
+  const uint32_t n_min = (none || pmax >= KP) ? 0u : div_small(KP - pmax, pmax, fast_rcp((float)pmax));
+  if (!live) return;
+  const uint32_t D = slow ? (uint32_t)(p2 - Vs) : 0u;
+#pragma unroll
+  for (uint32_t q = 0; q < 8; ++q) {
+    const uint32_t pl = (pl_rot >> (3 * q)) & 7u;
+    const uint32_t t = o.a[q] - Kbm - ((e_rot >> q) & 1u);
+    uint32_t kk = min(t, t + p);  // (a - Kb - e) mod p
+    if (slow) {
+      const uint32_t rho = (uint32_t)(rho_pack >> (5 * pl)) & 31u;
+      const uint32_t kmin = kmin_for(D, rho);
+      if (kmin > kk) {
+        const uint32_t d = kmin - kk;  // < 2^18
+        uint32_t qd = (uint32_t)((float)d * invp);
+        while (qd * p < d) ++qd;
+        while (qd > 0 && (qd - 1) * p >= d) --qd;
+        kk += qd * p;
+      }
+    }
+    uint32_t* const pb = seg + 8 * pl;
+#pragma unroll 2
+    for (uint32_t h = 0; h < n_min; ++h) {
+      lds_or(pb + ((kk >> 5) & (ROWS - 1)) * 64 + (kk >> LOG_LS), 1u << (kk & 31));
+      kk = opaque(kk + p);
+    }
+    for (; kk < KP; kk += p) lds_or(pb + ((kk >> 5) & (ROWS - 1)) * 64 + (kk >> LOG_LS), 1u << (kk & 31));
+  }
+}
+
+struct WheelLds {
+  uint32_t seg[KP * 8 / 32];       // the segment image (128 KiB)
+  uint64_t mid_m[kMidCap];         // Barrett factors of the staged mid primes
+  uint32_t mid_p[kMidCap];         // p | (30^{-1} mod p) << 16
+  uint32_t lut[256];               // period byte -> 15 odd slots
+  uint32_t thr[3];
+  unsigned long long wave_cnt[NW];
+};
+
 __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restrict__ table, WheelArgs wa,
                                                             uint32_t* __restrict__ out,
                                                             unsigned long long* __restrict__ count_out) {
-  __shared__ __attribute__((aligned(16))) uint32_t seg[KP * 8 / 32];
-  __shared__ uint64_t s_mid_m[kMidCap];
-  __shared__ uint32_t s_mid_p[kMidCap];
-  __shared__ uint32_t s_lut[256];
-  __shared__ uint32_t s_ctr;
-  __shared__ uint32_t s_thr[3];
-  __shared__ unsigned long long s_wave_cnt[NW];
+  // One static LDS object, so the segment image sits at LDS address 0
+  // (mark_col combines row and column offsets with a bitwise or).
+  __shared__ WheelLds lds;
+  uint32_t* const seg = lds.seg;
+  uint64_t* const s_mid_m = lds.mid_m;
+  uint32_t* const s_mid_p = lds.mid_p;
+  uint32_t* const s_lut = lds.lut;
+  uint32_t* const s_thr = lds.thr;
+  unsigned long long* const s_wave_cnt = lds.wave_cnt;
 
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
   const uint32_t np = th->count;
@@ -239,7 +453,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   const uint32_t* __restrict__ A =
       reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + table_a_offset(th->cap));
 
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t tid = threadIdx.x, lane_id = tid & 63, wave = tid >> 6;
   const uint32_t phases = wa.phases;
 
   if (tid == 0) {
@@ -266,18 +480,21 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   __syncthreads();
   const uint32_t i_mid0 = s_thr[0], i_midB = s_thr[1], i_mid1 = s_thr[2];
   for (uint32_t i = tid; i < i_mid1 - i_mid0; i += NT) {
-    s_mid_p[i] = P[i_mid0 + i];
+    const uint32_t q = P[i_mid0 + i];
+    s_mid_p[i] = q | ((uint32_t)inv30_of(q) << 16);  // p < 2^14, 30^{-1} mod p < p
     s_mid_m[i] = M[i_mid0 + i];
   }
-  // work units: S1 = nA single mid primes + nB diagonal units (8 primes each),
-  // S2 = nL large units (64 primes each); S1 and S2 interleaved
+  // Work units: list 1 = nA single mid primes, then nB diagonal units (8
+  // primes each); list 2 = nL large units (64 primes each). Round r of wave w
+  // takes unit r*16 + w (r even) or r*16 + 15 - w (r odd) of BOTH lists, so
+  // every wave gets the same mix of LDS-bound and latency-bound units and a
+  // balanced share of the sorted (cost ~ 1/p) lists. No atomics, no drains.
   const uint32_t nA = i_midB - i_mid0;
   const uint32_t n_mid = i_mid1 - i_mid0;
   const uint32_t nB = (i_mid1 - i_midB + 7) / 8;
   const uint32_t nL = (np - i_mid1 + 63) / 64;
-  const uint32_t nS1 = nA + nB, nS2 = nL;
-  const uint32_t nI = min(nS1, nS2);
-  const uint32_t n_units = nS1 + nS2;
+  const uint32_t n1 = nA + nB, n2 = nL;
+  const uint32_t n_rounds = (max(n1, n2) + NW - 1) / NW;
 
   const uint64_t out_words = 2ull * ((wa.nbits + 63) / 64);  // 32-bit words of the caller's mask
   const uint64_t nseg = (wa.nbits + kWheelOutBits - 1) / kWheelOutBits;
@@ -286,6 +503,10 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   for (uint64_t s = blockIdx.x; s < nseg; s += gridDim.x) {
     const uint64_t Vs = wa.V0 + s * kWheelSpan;  // segment base value
     const uint64_t Vend = Vs + kWheelSpan;
+    // Lane-derived values are segment-invariant; left visible, the compiler
+    // hoists dozens of them out of this loop and spills them. Recompute instead.
+    uint32_t lane = lane_id;
+    asm volatile("" : "+v"(lane));
 
     // ---- 1. init: small-prime patterns (7..61) -------------------------
     {
@@ -319,204 +540,79 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         seg[(r0 + r) * 64 + C] = (uint32_t)w;
         seg[(r0 + r + 1) * 64 + C] = (uint32_t)(w >> 32);
       }
-      if (tid == 0) s_ctr = 0;
     }
     __syncthreads();
 
     // ---- 2. mark -------------------------------------------------------
-    for (;;) {
-      uint32_t u = 0;
-      if (lane == 0) u = atomicAdd(&s_ctr, 1u);
-      u = __builtin_amdgcn_readlane(u, 0);
-      if (u >= n_units) break;
-      bool in_s1;
-      uint32_t k;
-      if (u < 2 * nI) { in_s1 = !(u & 1); k = u >> 1; }
-      else { in_s1 = nS1 > nS2; k = u - nI; }
-
-      if (in_s1 && k < nA) {
-        if (!(phases & kPhaseMidA)) continue;
-        // one prime per wave; lane L = column L = (plane L>>3, column L&7)
-        const uint32_t p = __builtin_amdgcn_readfirstlane(s_mid_p[k]);
-        const uint64_t p2 = (uint64_t)p * p;
-        if (p2 >= Vend) continue;
-        const uint64_t m = s_mid_m[k];
-        const uint32_t Xs = mod_barrett(Vs, p, m);
-        const float invp = fast_rcp((float)p);
-        const uint32_t pl = lane >> 3, c = lane & 7;
-        const uint32_t rho = (uint32_t)(wa.rho_pack >> (5 * pl)) & 31u;
-        const uint32_t kp = plane_first(Xs, rho, p, (uint32_t)inv30_of(p), invp);
-        uint32_t* const colp = seg + lane;
-        if (p2 <= Vs) {
-          const uint32_t cm = mod_small(c * LS, p, invp);
-          uint32_t off = kp >= cm ? kp - cm : kp + p - cm;
-          const uint32_t n_full = div_small(LS, p, invp);
-#pragma unroll 4
-          for (uint32_t h = 0; h < n_full; ++h) {
-            lds_or(colp + ((off >> 5) << 6), 1u << (off & 31));
-            off += p;
-          }
-          if (off < LS) lds_or(colp + ((off >> 5) << 6), 1u << (off & 31));
-        } else {
-          const uint32_t kmin = kmin_for((uint32_t)(p2 - Vs), rho);
-          const uint32_t kf = first_at_or_after(kp, max(kmin, c * LS), p, invp);
-          for (uint32_t off = kf - c * LS; off < LS; off += p) lds_or(colp + ((off >> 5) << 6), 1u << (off & 31));
-        }
-      } else if (in_s1) {
-        if (!(phases & kPhaseMidB)) continue;
-        // 8 primes x 8 planes: half-wave g takes planes 4g..4g+3; lane
-        // (prime jp, plane pl) walks columns jp, jp+1, ... (mod 8)
-        const uint32_t j0 = nA + (k - nA) * 8;
-        const uint32_t nj = min(8u, n_mid - j0);
-        const uint32_t pfirst = __builtin_amdgcn_readfirstlane(s_mid_p[j0]);
-        if ((uint64_t)pfirst * pfirst >= Vend) continue;
-        const uint32_t l = lane & 31;
-        const uint32_t pl = 4 * (lane >> 5) + (l & 3), jp = l >> 2;
-        const bool valid = jp < nj;
-        const uint32_t p = valid ? s_mid_p[j0 + jp] : pfirst;
-        const uint64_t m = s_mid_m[valid ? j0 + jp : j0];
-        const float invp = fast_rcp((float)p);
-        const uint32_t rho = (uint32_t)(wa.rho_pack >> (5 * pl)) & 31u;
-        const uint32_t Xs = mod_barrett(Vs, p, m);
-        const uint32_t kp = plane_first(Xs, rho, p, (uint32_t)inv30_of(p), invp);
-        const uint64_t p2 = (uint64_t)p * p;
-        uint32_t O0, off;
-        const uint32_t cstart = jp * LS;
-        const bool slow = p2 > Vs;
-        if (!slow) {
-          O0 = kp;
-          const uint32_t cm = mod_small(cstart, p, invp);
-          off = kp >= cm ? kp - cm : kp + p - cm;
-        } else {
-          const uint32_t kmin = p2 >= Vend ? KP : kmin_for((uint32_t)(p2 - Vs), rho);
-          O0 = first_at_or_after(kp, kmin, p, invp);
-          off = first_at_or_after(kp, max(kmin, cstart), p, invp) - cstart;
-        }
-        const uint32_t pmin = pfirst;
-        const uint32_t pmax = __builtin_amdgcn_readfirstlane(s_mid_p[j0 + nj - 1]);
-        const bool any_slow = __builtin_amdgcn_ballot_w64(slow) != 0;
-        const uint32_t n_u = any_slow ? 0u : div_small(LS, pmax, fast_rcp((float)pmax));
-        const uint32_t n_x = div_ceil_small(LS, pmin, fast_rcp((float)pmin)) - n_u;
-        const uint32_t cb = 8 * pl;
-        // lanes past the batch end mark nothing (their unconditional marks would
-        // land in another prime's columns)
-        if (!valid) {
-        } else if (n_u >= 1 && n_u <= 15 && n_x >= 1 && n_x <= 2) {
-          diag_dispatch<1>(n_u, n_x, seg, off, p, cb, jp, O0);
-        } else {
-          uint32_t c = jp;
-          for (uint32_t t = 0; t < 8; ++t) {
-            uint32_t* colp = seg + cb + c;
-            for (uint32_t h = 0; h < n_u; ++h) {
-              lds_or(colp + ((off >> 5) << 6), 1u << (off & 31));
-              off += p;
-            }
-            for (uint32_t h = 0; h < n_x; ++h) {
-              const bool hit = off < LS;
-              const uint32_t o = hit ? off : 0u;
-              lds_or(colp + ((o >> 5) << 6), hit ? 1u << (o & 31) : 0u);
-              off = hit ? off + p : off;
-            }
-            off -= LS;
-            c = (c + 1) & 7;
-            off = c == 0 ? O0 : off;
+    if (phases & kPhaseUnits) {
+      const uint32_t rot = (i_mid1 + lane) & 7;  // = table index & 7 of this lane's large primes
+      // absolute residue (q + rot) & 7 at step q: its plane and e bit
+      const uint32_t pl_rot = ((wa.pl_pack >> (3 * rot)) | (wa.pl_pack << (24 - 3 * rot))) & 0xFFFFFFu;
+      const uint32_t e_rot = ((wa.e_iota >> rot) | (wa.e_iota << (8 - rot))) & 0xFFu;
+      const uint64_t Kb = wa.KB0 + s * (uint64_t)KP;
+      LargeOps nxt;
+      auto l_index = [&](uint32_t r) { return (r & 1) ? r * NW + (NW - 1 - wave) : r * NW + wave; };
+      if (l_index(0) < n2) load_L(nxt, P, M, A, i_mid1 + 64 * l_index(0) + lane, np);
+      for (uint32_t r = 0; r < n_rounds; ++r) {
+        const uint32_t u = l_index(r);
+        if (u < n1) {
+          if (u < nA) {
+            const uint32_t pi = __builtin_amdgcn_readfirstlane(s_mid_p[u]);
+            const uint32_t p = pi & 0xFFFFu;
+            const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mid_m[u] >> 32)) << 32) |
+                               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_mid_m[u]);  // (int -> no sign extension)
+            if ((phases & kPhaseMidA) && (uint64_t)p * p < Vend) unit_A(seg, pi, m, Vs, wa.rho_pack, lane);
+          } else {
+            const uint32_t j0 = nA + (u - nA) * 8;
+            const uint32_t pf = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
+            if ((phases & kPhaseMidB) && (uint64_t)pf * pf < Vend)
+              unit_B(seg, s_mid_p, s_mid_m, j0, min(8u, n_mid - j0), Vs, Vend, wa.rho_pack, lane);
           }
         }
-      } else {
-        if (!(phases & kPhaseLarge)) continue;
-        // 64 primes > LS, one per lane, planes in a lane-rotated order
-        const uint32_t base = i_mid1 + k * 64;
-        const uint32_t p0 = __builtin_amdgcn_readfirstlane(P[base]);
-        if ((uint64_t)p0 * p0 >= Vend) continue;
-        const uint32_t il = base + lane;
-        const bool ok = il < np;
-        const uint32_t p = ok ? P[il] : 0x7FFFFFFFu;
-        const uint64_t m = ok ? M[il] : 1ull;
-        const uint64_t p2 = (uint64_t)p * p;
-        const bool live = ok && p2 < Vend;
-        const bool slow = p2 > Vs;
-        const uint32_t D = slow && live ? (uint32_t)(p2 - Vs) : 0u;
-        const uint64_t Kb = wa.KB0 + s * (uint64_t)KP;
-        const uint32_t Kbm = ok ? mod_barrett(Kb, p, m) : 0u;
-        const float invp = fast_rcp((float)p);
-        const uint32_t pmax = __builtin_amdgcn_readlane(p, 63);
-        const bool none = __builtin_amdgcn_ballot_w64(!live || slow) != 0;
-        const uint32_t n_min = (none || pmax >= KP) ? 0u : div_small(KP - pmax, pmax, fast_rcp((float)pmax));
-        uint32_t av[8];
-#pragma unroll
-        for (uint32_t q = 0; q < 8; ++q) {
-          const uint32_t pl = (q + lane) & 7;
-          av[q] = live ? A[8ull * il + ((wa.iota_pack >> (3 * pl)) & 7u)] : 0u;
-        }
-        if (live) {
-#pragma unroll
-          for (uint32_t q = 0; q < 8; ++q) {
-            const uint32_t pl = (q + lane) & 7;
-            const uint32_t e = (wa.e_bits >> pl) & 1u;
-            int32_t kr = (int32_t)av[q] - (int32_t)Kbm - (int32_t)e;
-            kr = kr < 0 ? kr + (int32_t)p : kr;
-            kr = kr < 0 ? kr + (int32_t)p : kr;
-            uint32_t kk = (uint32_t)kr;
-            if (slow) {
-              const uint32_t rho = (uint32_t)(wa.rho_pack >> (5 * pl)) & 31u;
-              const uint32_t kmin = kmin_for(D, rho);
-              if (kmin > kk) {
-                const uint32_t d = kmin - kk;  // < 2^18
-                uint32_t qd = (uint32_t)((float)d * invp);
-                while (qd * p < d) ++qd;
-                while (qd > 0 && (qd - 1) * p >= d) --qd;
-                kk += qd * p;
-              }
-            }
-            uint32_t* const pb = seg + 8 * pl;
-#pragma unroll 2
-            for (uint32_t h = 0; h < n_min; ++h) {
-              lds_or(pb + ((kk >> 5) & (ROWS - 1)) * 64 + (kk >> LOG_LS), 1u << (kk & 31));
-              kk += p;
-            }
-            for (; kk < KP; kk += p) lds_or(pb + ((kk >> 5) & (ROWS - 1)) * 64 + (kk >> LOG_LS), 1u << (kk & 31));
-          }
+        if (u < n2) {
+          const LargeOps cur = nxt;
+          const uint32_t un = l_index(r + 1);
+          if (un < n2) load_L(nxt, P, M, A, i_mid1 + 64 * un + lane, np);  // prefetch
+          const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p);
+          if ((phases & kPhaseLarge) && (uint64_t)p0 * p0 < Vend) unit_L(seg, cur, Vs, Vend, Kb, pl_rot, e_rot, wa.rho_pack);
         }
       }
     }
+    lds_drain();
     __syncthreads();
 
     // ---- 3. expand to odd-only bits, count, store ------------------------
-    {
+    if (phases & kPhaseExpand) {
       const uint32_t c = lane >> 3, a8 = lane & 7;
       const uint64_t seg_word0 = s * (uint64_t)kOutWordsPerSeg;
 #pragma unroll 1
       for (uint32_t t = 0; t < ROWS / (NW * 8); ++t) {
         const uint32_t row = 8 * ((ROWS / (NW * 8)) * wave + t) + a8;
         const uint32_t* rp = seg + row * 64 + c;
-        uint32_t Pw[8];
+        uint32_t Q[8];
 #pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) Pw[j] = ~rp[8 * ((j + a8) & 7)];  // plane (j + a8) & 7, 1 = prime
-        // un-rotate: plane i = Pw[(i - a8) & 7]
+        for (uint32_t j = 0; j < 8; ++j) Q[j] = ~rp[8 * ((j + a8) & 7)];  // plane (j + a8) & 7, 1 = prime
+        // un-rotate by a8 (plane i = Q[(i - a8) & 7]): three conditional rotations
+        uint32_t R1[8], R2[8], Pw[8];
 #pragma unroll
-        for (uint32_t b = 1; b < 8; b <<= 1) {
-          uint32_t T[8];
+        for (int i = 0; i < 8; ++i) R1[i] = (a8 & 1) ? Q[(i + 7) & 7] : Q[i];
 #pragma unroll
-          for (uint32_t i = 0; i < 8; ++i) T[i] = (a8 & b) ? Pw[(i - b) & 7] : Pw[i];
+        for (int i = 0; i < 8; ++i) R2[i] = (a8 & 2) ? R1[(i + 6) & 7] : R1[i];
 #pragma unroll
-          for (uint32_t i = 0; i < 8; ++i) Pw[i] = T[i];
-        }
+        for (int i = 0; i < 8; ++i) Pw[i] = (a8 & 4) ? R2[(i + 4) & 7] : R2[i];
+        uint32_t TL[4], TH[4];
+        byte_transpose4(Pw, TL);
+        byte_transpose4(Pw + 4, TH);
         uint32_t o[15];
 #pragma unroll
         for (int w = 0; w < 15; ++w) o[w] = 0;
 #pragma unroll
-        for (uint32_t q = 0; q < 4; ++q) {
-          uint32_t lo = 0, hi = 0;
+        for (int q = 0; q < 4; ++q) {
+          const uint64_t x = transpose8((uint64_t)TL[q] | ((uint64_t)TH[q] << 32));
 #pragma unroll
-          for (uint32_t i = 0; i < 4; ++i) {
-            lo |= ((Pw[i] >> (8 * q)) & 0xFFu) << (8 * i);
-            hi |= ((Pw[i + 4] >> (8 * q)) & 0xFFu) << (8 * i);
-          }
-          const uint64_t x = transpose8((uint64_t)lo | ((uint64_t)hi << 32));
-#pragma unroll
-          for (uint32_t bb = 0; bb < 8; ++bb) {
+          for (int bb = 0; bb < 8; ++bb) {
             const uint32_t e = s_lut[(uint32_t)(x >> (8 * bb)) & 0xFFu];
-            const uint32_t pos = 15 * (8 * q + bb);
+            const int pos = 15 * (8 * q + bb);
             o[pos >> 5] |= e << (pos & 31);
             if ((pos & 31) > 17) o[(pos >> 5) + 1] |= e >> (32 - (pos & 31));
           }
@@ -524,15 +620,18 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         const uint64_t w0 = seg_word0 + 15ull * (c * ROWS + row);  // caller's 32-bit word index
         if (s == 0 && c == 0 && row == 0) o[0] |= wa.fix0;
         const uint64_t bit0 = 32ull * w0;
-        if (bit0 + 480 > wa.nbits) {
+        if (bit0 + 480 > wa.nbits) {  // range end (last segment only)
+          const uint32_t rem = bit0 >= wa.nbits ? 0u : (uint32_t)(wa.nbits - bit0);  // < 480 valid bits
 #pragma unroll
           for (int w = 0; w < 15; ++w) {
-            const uint64_t b = bit0 + 32ull * w;
-            o[w] = b >= wa.nbits ? 0u : (wa.nbits - b >= 32 ? o[w] : o[w] & ((1u << (wa.nbits - b)) - 1u));
+            const uint32_t b = 32u * w;
+            o[w] = b >= rem ? 0u : (rem - b >= 32 ? o[w] : o[w] & ((1u << (rem - b)) - 1u));
           }
         }
+        uint32_t cnt = 0;
 #pragma unroll
-        for (int w = 0; w < 15; ++w) my_count += (unsigned long long)__popc(o[w]);
+        for (int w = 0; w < 15; ++w) cnt += __popc(o[w]);
+        my_count += cnt;
         if (out && (phases & kPhaseStore)) {
           if (w0 + 15 <= out_words) {
 #pragma unroll
@@ -550,7 +649,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
 
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) my_count += __shfl_xor(my_count, o);
-  if (lane == 0) s_wave_cnt[wave] = my_count;
+  if (lane_id == 0) s_wave_cnt[wave] = my_count;
   __syncthreads();
   if (tid == 0) {
     unsigned long long t = 0;
@@ -579,7 +678,7 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
     for (int j = 0; j < 8; ++j) {
       const uint32_t t = kR30[j] % p;
       const uint32_t u = t ? p - t : 0u;
-      A[8ull * i + j] = mod_barrett((uint64_t)u * inv, p, m);
+      A[8ull * i + ((j - i) & 7)] = mod_barrett((uint64_t)u * inv, p, m);  // row rotated by i & 7
     }
   }
 }
@@ -611,8 +710,8 @@ hipError_t launch_sieve_range_wheel(const void* table, uint64_t g_start, uint64_
     uint32_t iota = 0;
     while (kR30[iota] != r) ++iota;
     wa.rho_pack |= (uint64_t)rho << (5 * n);
-    wa.iota_pack |= iota << (3 * n);
-    if (v0m + rho >= 30) wa.e_bits |= 1u << n;
+    wa.pl_pack |= n << (3 * iota);
+    if (v0m + rho >= 30) wa.e_iota |= 1u << iota;
     ++n;
   }
   if (n != 8) return hipErrorInvalidValue;

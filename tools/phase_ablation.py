@@ -3,8 +3,10 @@ process per variant is avoided by re-exec-free subprocess runs. Profiling only."
 import os, subprocess, sys, json
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 N = sys.argv[1] if len(sys.argv) > 1 else "1e11"
-variants = {"all": 63, "no_store": 47, "no_small": 55, "only_midA": 1 | 16, "only_midB": 2 | 16,
-            "only_coopC": 4 | 16, "only_scatterD": 32 | 16, "only_small": 8 | 16, "only_zero_wb": 16, "nothing": 0}
+# wheel kernel phases: 1 = A, 2 = B, 4 = L, 8 = patterns (init), 16 = store, 32 = expand, 64 = unit loop
+variants = {"all": 127, "no_store": 111, "only_A": 1 | 120, "only_B": 2 | 120, "only_L": 4 | 120,
+            "init_units_expand_store": 120, "init_units_expand": 104, "init_units": 72, "init_expand": 40,
+            "init": 8, "nothing": 0}
 for name, ph in variants.items():
     env = dict(os.environ, DSE_PHASES=str(ph))
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "5", "--warmup", "2",

@@ -5,6 +5,6 @@ for d in sorted(glob.glob(os.path.join(root, "*/"))):
     if not f: continue
     agg = collections.defaultdict(list)
     for r in csv.DictReader(open(f[0])):
-        if "sieve_segments" in r["Kernel_Name"]:
+        if "segments_kernel" in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
     print(os.path.basename(d.rstrip("/")), " ".join(f"{k}={sum(v)/len(v):.3e}" for k, v in sorted(agg.items())))
