@@ -53,7 +53,12 @@ constexpr uint32_t ROWS = LS / 32;          // 512 words per column
 constexpr uint32_t NT = 1024;
 constexpr uint32_t NW = NT / 64;
 constexpr uint32_t TA = LS / 16;            // A/B threshold
-constexpr uint32_t kMidCap = 1920;          // odd primes in (61, LS]: 1882
+#ifndef DSE_TB
+#define DSE_TB 8192
+#endif
+constexpr uint32_t TB = DSE_TB;             // B/L threshold (<= LS)
+static_assert(TB <= LS && TB >= TA, "B/L threshold");
+constexpr uint32_t kMidCap = TB >= 16384 ? 1920 : TB >= 8192 ? 1040 : TB >= 4096 ? 580 : 320;  // odd primes in (61, TB]
 constexpr uint32_t kOutWordsPerSeg = (uint32_t)(kWheelOutBits / 32);  // 61440
 
 constexpr int kNQ = 15;
@@ -373,17 +378,39 @@ struct LargeOps {
 
 __device__ __forceinline__ void load_L(LargeOps& o, const uint32_t* __restrict__ P, const uint64_t* __restrict__ M,
                                        const uint32_t* __restrict__ A, uint32_t il, uint32_t np) {
-  const bool ok = il < np;
-  o.p = ok ? P[il] : 0x7FFFFFFFu;
-  o.m = ok ? M[il] : 1ull;
-  const uint4* row = reinterpret_cast<const uint4*>(A + 8ull * il);
-  const uint4 lo = ok ? row[0] : make_uint4(0, 0, 0, 0), hi = ok ? row[1] : make_uint4(0, 0, 0, 0);
+  const uint32_t ic = min(il, np - 1);  // past the table end: load the last row, mark nothing
+  o.p = il < np ? P[ic] : 0x7FFFFFFFu;
+  o.m = M[ic];
+  const uint4* row = reinterpret_cast<const uint4*>(A + 8ull * ic);
+  const uint4 lo = row[0], hi = row[1];
   o.a[0] = lo.x; o.a[1] = lo.y; o.a[2] = lo.z; o.a[3] = lo.w;
   o.a[4] = hi.x; o.a[5] = hi.y; o.a[6] = hi.z; o.a[7] = hi.w;
 }
 
-// L: 64 large primes (p > LS), one per lane; at step q lane L handles the
-// absolute residue (q + L) & 7, so a half-wave spreads over all 8 planes.
+// Mark plane-relative period kk of plane byte base pb32 = lds0 + 32 * plane:
+// word (row (kk >> 5) & 511, column 8 * plane + ((kk >> 14) & 7)). The masks
+// keep any kk inside the segment, so a predicated-off mark (PRED and kk >= KP)
+// is an OR of 0 at a valid address. asm for the same reason as mark_col.
+template <bool PRED>
+__device__ __forceinline__ void mark_plane(uint32_t pb32, uint32_t kk) {
+  const uint32_t col = __builtin_amdgcn_ubfe(kk, 14, 3);
+  uint32_t bit = 1u << (kk & 31);
+  if (PRED) bit = kk < KP ? bit : 0u;
+  uint32_t a, t;
+  asm volatile(
+      "v_lshl_or_b32 %1, %2, 2, %3\n\t"
+      "v_lshlrev_b32 %0, 3, %4\n\t"
+      "v_and_or_b32 %0, %0, %5, %1\n\t"
+      "ds_or_b32 %0, %6"
+      : "=&v"(a), "=&v"(t)
+      : "v"(col), "v"(pb32), "v"(kk), "s"(0x1FF00u), "v"(bit)
+      : "memory");
+}
+
+// L: 64 large primes (p > TB), one per lane; at step q lane L handles the
+// absolute residue (q + L) & 7 (a half-wave spreads over all 8 planes). The
+// per-plane hit count is at most ceil(KP / pmin): units whose primes all
+// exceed KP (resp. KP/2) take one (two) predicated marks per plane, no loop.
 __device__ __forceinline__ void unit_L(uint32_t* __restrict__ seg, const LargeOps& o, uint64_t Vs, uint64_t Vend,
                                        uint64_t Kb, uint32_t pl_rot, uint32_t e_rot, uint64_t rho_pack) {
   const uint32_t p = o.p;
@@ -391,16 +418,18 @@ __device__ __forceinline__ void unit_L(uint32_t* __restrict__ seg, const LargeOp
   const bool live = p2 < Vend;
   const bool slow = p2 > Vs;
   const uint32_t Kbm = mod_barrett(Kb, p, o.m);
+  const uint32_t Kbm1 = Kbm + 1;
   const float invp = fast_rcp((float)p);
+  const uint32_t pmin = __builtin_amdgcn_readfirstlane(p);
   const uint32_t pmax = __builtin_amdgcn_readlane(p, 63);
   const bool none = __builtin_amdgcn_ballot_w64(!live || slow) != 0;
   const uint32_t n_min = (none || pmax >= KP) ? 0u : div_small(KP - pmax, pmax, fast_rcp((float)pmax));
-  if (!live) return;
-  const uint32_t D = slow ? (uint32_t)(p2 - Vs) : 0u;
+  const uint32_t D = slow && live ? (uint32_t)(p2 - Vs) : 0u;
+  const uint32_t lds0 = lds_addr(seg);
 #pragma unroll
   for (uint32_t q = 0; q < 8; ++q) {
     const uint32_t pl = (pl_rot >> (3 * q)) & 7u;
-    const uint32_t t = o.a[q] - Kbm - ((e_rot >> q) & 1u);
+    const uint32_t t = o.a[q] - (((e_rot >> q) & 1u) ? Kbm1 : Kbm);
     uint32_t kk = min(t, t + p);  // (a - Kb - e) mod p
     if (slow) {
       const uint32_t rho = (uint32_t)(rho_pack >> (5 * pl)) & 31u;
@@ -413,13 +442,21 @@ __device__ __forceinline__ void unit_L(uint32_t* __restrict__ seg, const LargeOp
         kk += qd * p;
       }
     }
-    uint32_t* const pb = seg + 8 * pl;
+    kk = live ? kk : KP;
+    const uint32_t pb32 = lds0 + 32 * pl;
+    if (pmin > KP) {
+      mark_plane<true>(pb32, kk);
+    } else if (pmin > KP / 2) {
+      mark_plane<true>(pb32, kk);
+      mark_plane<true>(pb32, kk + p);
+    } else {
 #pragma unroll 2
-    for (uint32_t h = 0; h < n_min; ++h) {
-      lds_or(pb + ((kk >> 5) & (ROWS - 1)) * 64 + (kk >> LOG_LS), 1u << (kk & 31));
-      kk = opaque(kk + p);
+      for (uint32_t h = 0; h < n_min; ++h) {
+        mark_plane<false>(pb32, kk);
+        kk = opaque(kk + p);
+      }
+      for (; kk < KP; kk += p) mark_plane<false>(pb32, kk);
     }
-    for (; kk < KP; kk += p) lds_or(pb + ((kk >> 5) & (ROWS - 1)) * 64 + (kk >> LOG_LS), 1u << (kk & 31));
   }
 }
 
@@ -457,7 +494,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   const uint32_t phases = wa.phases;
 
   if (tid == 0) {
-    // first index with p > 61, with p > TA, with p > LS (capped by the LDS stage)
+    // first index with p > 61, with p > TA, with p > TB (capped by the LDS stage)
     uint32_t lo = 0, hi = np;
     while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= kQMax) lo = mid + 1; else hi = mid; }
     s_thr[0] = lo;
@@ -465,7 +502,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= TA) lo = mid + 1; else hi = mid; }
     s_thr[1] = lo;
     hi = np;
-    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= LS) lo = mid + 1; else hi = mid; }
+    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= TB) lo = mid + 1; else hi = mid; }
     s_thr[2] = min(lo, s_thr[0] + kMidCap);
   }
   if (tid < 256) {

@@ -10,4 +10,4 @@ for rnd in range(2):
         if r.returncode:
             print(v, "FAILED", r.stderr[-400:]); sys.exit(1)
         j = json.loads(r.stdout.strip().splitlines()[-1])
-        print(rnd, v, f"kernel_ms={j['roofline']['kernel_ms']:.3f} ok={j['verified']}", flush=True)
+        print(rnd, v, "kernel_ms=%.3f ok=%s" % (j['roofline']['kernel_ms'], j['verified']), flush=True)
