@@ -61,26 +61,35 @@ def cpu_baseline(sample_n: int) -> dict:
                       "the Clojure reference cannot run (no JVM in the image)"}
 
 
-def pmc_traffic(N: int, P: int):
-    """HBM bytes per sieve launch from the committed rocprofv3 PMC passes for
-    this config (profiles/<round>/pmc_{fetch,write}_sieve_kernel.csv, N=1e11,
-    P=1), with the gfx950 correction of MI355X_MICROARCH.md: FETCH_SIZE counts
-    half of a wide coalesced read, WRITE_SIZE is exact; both in KiB."""
+def pmc_summary(N: int, P: int):
+    """Per-launch figures of the sieve kernel from the committed rocprofv3 PMC
+    passes for this config (profiles/<round>/pmc_*_sieve_kernel.csv, N=1e11,
+    P=1): HBM bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB counters; MI355X_MICROARCH.md:
+    gfx950 FETCH_SIZE counts half of a wide coalesced read, WRITE_SIZE is exact),
+    and the VALU / LDS wave-instruction issue rates per CU per cycle
+    (GRBM_GUI_ACTIVE is summed over the 8 XCDs)."""
+    import collections
     import csv
     import glob
     if (N, P) != (10**11, 1):
-        return None, None
+        return None
     for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")), reverse=True):
         try:
-            vals = {}
-            for f, name in (("pmc_fetch_sieve_kernel.csv", "FETCH_SIZE"), ("pmc_write_sieve_kernel.csv", "WRITE_SIZE")):
-                rows = [float(r["Counter_Value"]) for r in csv.DictReader(open(os.path.join(d, f)))
-                        if r["Counter_Name"] == name]
-                vals[name] = sum(rows) / len(rows)
-            return (2 * vals["FETCH_SIZE"] + vals["WRITE_SIZE"]) * 1024, os.path.relpath(d, ROOT)
+            vals = collections.defaultdict(list)
+            for f in ("pmc_fetch_sieve_kernel.csv", "pmc_write_sieve_kernel.csv", "pmc_sq_sieve_kernel.csv",
+                      "pmc_wait_sieve_kernel.csv"):
+                for r in csv.DictReader(open(os.path.join(d, f))):
+                    if "wheel_segments_kernel" in r["Kernel_Name"]:
+                        vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            v = {k: sum(x) / len(x) for k, x in vals.items()}
+            cyc = v["GRBM_GUI_ACTIVE"] / 8
+            return {"traffic": (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024, "source": os.path.relpath(d, ROOT),
+                    "valu_issue_per_cu_cycle": v["SQ_INSTS_VALU"] / 256 / cyc,
+                    "lds_issue_per_cu_cycle": v["SQ_INSTS_LDS"] / 256 / cyc,
+                    "lds_conflict_cycle_share": v["SQ_LDS_BANK_CONFLICT"] / v["SQ_LDS_IDX_ACTIVE"]}
         except (OSError, KeyError, ZeroDivisionError):
             continue
-    return None, None
+    return None
 
 
 def main():
@@ -149,7 +158,7 @@ def main():
     T = elapsed.item()
     if rank == 0:
         rf = work.roofline(g0, cs, kern_t.item())
-        traffic, traffic_src = pmc_traffic(N, P) if not a.no_mask else (None, None)
+        pmc = pmc_summary(N, P) if not a.no_mask else None
         out = {
             "metric": METRIC,
             "value": N * a.steps / T,
@@ -173,9 +182,13 @@ def main():
             "roofline": {"bound": rf["bound"],
                          "achieved": rf["lds_achieved_gbs"] if rf["bound"] == "lds" else rf["hbm_achieved_gbs"],
                          "peak": work.LDS_PEAK_GBS if rf["bound"] == "lds" else work.HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": rf["frac"], "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "kernel": "sieve_segments_kernel<20,1024>", "kernel_ms": kern_t.item() * 1e3,
+                         "unit": "GB/s", "frac": rf["frac"], "traffic": pmc["traffic"] if pmc else None,
+                         "pmc_source": pmc["source"] if pmc else None,
+                         "wheel_marks_per_launch": rf["wheel_marks"], "frac_executed": rf["frac_executed"],
+                         "valu_issue_per_cu_cycle": pmc["valu_issue_per_cu_cycle"] if pmc else None,
+                         "lds_issue_per_cu_cycle": pmc["lds_issue_per_cu_cycle"] if pmc else None,
+                         "lds_conflict_cycle_share": pmc["lds_conflict_cycle_share"] if pmc else None,
+                         "kernel": "wheel_segments_kernel", "kernel_ms": kern_t.item() * 1e3,
                          "marks_per_launch": rf["marks"], "bytes_per_mark": work.BYTES_PER_MARK,
                          "hbm_bytes_per_launch": rf["hbm_bytes"], "hbm_achieved": rf["hbm_achieved_gbs"],
                          "hbm_peak": work.HBM_PEAK_GBS},

@@ -52,9 +52,41 @@ def marks_for_range(g_start: int, nbits: int) -> int:
     return int(cnt.sum())
 
 
+R30 = (1, 7, 11, 13, 17, 19, 23, 29)
+WHEEL_PATTERN_MAX = 61  # the wheel kernel ORs register patterns for 7..61 (no LDS marks)
+
+
+def _coprime30_upto(x: np.ndarray) -> np.ndarray:
+    """#{1 <= m <= x : gcd(m, 30) = 1} (x >= 0)."""
+    q, r = np.divmod(x, 30)
+    return 8 * q + np.searchsorted(np.array(R30), r, side="right")
+
+
+def wheel_marks_for_range(g_start: int, nbits: int) -> int:
+    """LDS marks the mod-30 wheel kernel issues for the odd-index range:
+    multiples p*m >= p^2 with gcd(m, 30) = 1 of every prime 61 < p <= sqrt(vmax)
+    (multiples of 3 and 5 are not stored, primes 7..61 are register patterns)."""
+    if nbits <= 0:
+        return 0
+    va = 3 + 2 * g_start
+    vb = 3 + 2 * (g_start + nbits - 1)
+    ps = odd_primes_upto(math.isqrt(vb))
+    ps = ps[ps > WHEEL_PATTERN_MAX]
+    if ps.size == 0:
+        return 0
+    lo = np.maximum(ps * ps, va)
+    m0 = (lo + ps - 1) // ps
+    m1 = vb // ps
+    cnt = np.where(m1 >= m0, _coprime30_upto(m1) - _coprime30_upto(m0 - 1), 0)
+    return int(cnt.sum())
+
+
 def roofline(g_start: int, nbits: int, seconds: float, launches: int = 1) -> dict:
-    """t_roof = max(8*marks/BW_LDS, (nbits/8)/BW_HBM)."""
+    """t_roof = max(8*marks/BW_LDS, (nbits/8)/BW_HBM), marks =
+    the algorithmic odd-only count. The wheel kernel issues fewer LDS marks
+    (wheel_marks): frac_executed prices those instead."""
     marks = marks_for_range(g_start, nbits)
+    wmarks = wheel_marks_for_range(g_start, nbits)
     lds_bytes = BYTES_PER_MARK * marks
     hbm_bytes = (nbits + 7) // 8
     t = seconds / launches
@@ -69,4 +101,6 @@ def roofline(g_start: int, nbits: int, seconds: float, launches: int = 1) -> dic
         "lds_achieved_gbs": lds_bytes / t / 1e9,
         "hbm_achieved_gbs": hbm_bytes / t / 1e9,
         "frac": max(t_lds, t_hbm) / t,
+        "wheel_marks": wmarks,
+        "frac_executed": max(BYTES_PER_MARK * wmarks / (LDS_PEAK_GBS * 1e9), t_hbm) / t,
     }
