@@ -205,23 +205,24 @@ __device__ __forceinline__ uint32_t kmin_for(uint32_t D, uint32_t rho) {
   return D > rho ? (D - rho + 29u) / 30u : 0u;
 }
 
-// 8 diagonal column steps of one lane's prime with compile-time hit counts:
-// NU unconditional marks and NX value-predicated ones per column; at the wrap
-// from column 7 back to column 0 the offset restarts at the plane start O0.
-template <int NU, int NX>
+// 8 diagonal column steps of one lane's prime: per column n_u unconditional
+// marks and n_x value-predicated ones (wave-uniform counts, so the loop
+// control runs on the scalar unit); at the wrap from column 7 back to column 0
+// the offset restarts at the plane start O0. One instance for every count:
+// compile-time variants (~28 touched per segment) cost more in
+// instruction-cache misses than they save.
 __device__ __forceinline__ void diag_walk(uint32_t* __restrict__ seg, uint32_t off, uint32_t p, uint32_t cb,
-                                          uint32_t c, uint32_t O0) {
-#pragma unroll 2
+                                          uint32_t c, uint32_t O0, uint32_t n_u, uint32_t n_x) {
+  const uint32_t lds0 = lds_addr(seg);
   for (uint32_t t = 0; t < 8; ++t) {
     uint32_t* colp = seg + cb + c;
-    const uint32_t cb_col = lds_addr(seg) + 4 * (cb + c);
-#pragma unroll
-    for (int h = 0; h < NU; ++h) {
+    const uint32_t cb_col = lds0 + 4 * (cb + c);
+#pragma unroll 2
+    for (uint32_t h = 0; h < n_u; ++h) {
       mark_col(cb_col, off);
       off = opaque(off + p);
     }
-#pragma unroll
-    for (int h = 0; h < NX; ++h) {
+    for (uint32_t h = 0; h < n_x; ++h) {
       const bool hit = off < LS;
       const uint32_t o = hit ? off : 0u;
       lds_or(colp + ((o >> 5) << 6), hit ? 1u << (o & 31) : 0u);
@@ -230,19 +231,6 @@ __device__ __forceinline__ void diag_walk(uint32_t* __restrict__ seg, uint32_t o
     off -= LS;
     c = (c + 1) & 7;
     off = c == 0 ? O0 : off;
-  }
-}
-
-template <int U>
-__device__ __forceinline__ void diag_dispatch(uint32_t n_u, uint32_t n_x, uint32_t* __restrict__ seg, uint32_t off,
-                                              uint32_t p, uint32_t cb, uint32_t c, uint32_t O0) {
-  if constexpr (U <= 15) {
-    if (n_u == U) {
-      if (n_x == 1) diag_walk<U, 1>(seg, off, p, cb, c, O0);
-      else diag_walk<U, 2>(seg, off, p, cb, c, O0);
-      return;
-    }
-    diag_dispatch<U + 1>(n_u, n_x, seg, off, p, cb, c, O0);
   }
 }
 
@@ -343,28 +331,7 @@ __device__ __forceinline__ void unit_B(uint32_t* __restrict__ seg, const uint32_
   // lanes past the batch end mark nothing (their unconditional marks would
   // land in another prime's columns)
   if (!valid) return;
-  if (n_u >= 1 && n_u <= 15 && n_x >= 1 && n_x <= 2) {
-    diag_dispatch<1>(n_u, n_x, seg, off, p, cb, jp, O0);
-    return;
-  }
-  uint32_t c = jp;
-  for (uint32_t t = 0; t < 8; ++t) {
-    uint32_t* colp = seg + cb + c;
-    const uint32_t cb_col = lds_addr(seg) + 4 * (cb + c);
-    for (uint32_t h = 0; h < n_u; ++h) {
-      mark_col(cb_col, off);
-      off += p;
-    }
-    for (uint32_t h = 0; h < n_x; ++h) {
-      const bool hit = off < LS;
-      const uint32_t o = hit ? off : 0u;
-      lds_or(colp + ((o >> 5) << 6), hit ? 1u << (o & 31) : 0u);
-      off = hit ? off + p : off;
-    }
-    off -= LS;
-    c = (c + 1) & 7;
-    off = c == 0 ? O0 : off;
-  }
+  diag_walk(seg, off, p, cb, jp, O0, n_u, n_x);
 }
 
 // Operands of one large unit, loaded ahead of use. The table row of prime i

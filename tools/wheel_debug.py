@@ -44,6 +44,6 @@ if __name__ == "__main__":
     if len(sys.argv) > 3:
         run_one(g0, nb, int(sys.argv[3]))
         sys.exit(0)
-    for ph in (16 | 96, 24 | 96, 25 | 96, 26 | 96, 28 | 96, 127):
+    for ph in (24 | 96, 25 | 96, 26 | 96, 28 | 96, 127):
         env = dict(os.environ, DSE_PHASES=str(ph), DSE_KERNEL="wheel")
         subprocess.run([sys.executable, __file__, str(g0), str(nb), str(ph)], env=env, timeout=120)
