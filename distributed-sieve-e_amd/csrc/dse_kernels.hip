@@ -22,6 +22,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "dse_internal.h"
 
 namespace dse {
@@ -496,89 +498,14 @@ __global__ __launch_bounds__(NT) void sieve_segments_kernel(const void* __restri
 }
 
 // ---------------------------------------------------------------------------
-// Base primes: every odd prime <= limit into the table, one workgroup.
-// ---------------------------------------------------------------------------
-constexpr uint32_t kBaseWords = 150u * 256u;  // 150 KiB of LDS bits (odd values)
-
-__global__ __launch_bounds__(1024) void base_primes_kernel(uint64_t limit, void* __restrict__ table, uint32_t cap) {
-  __shared__ uint32_t bm[kBaseWords];      // 1 = odd index g (value 3+2g) is composite
-  __shared__ uint32_t s_scan[1024];
-  __shared__ uint8_t s_isp[1024];         // primality of the sieving primes q = 3+2t <= sqrt(limit)
-  const uint32_t tid = threadIdx.x;
-  const uint32_t nb = limit >= 3 ? (uint32_t)((limit - 3) / 2 + 1) : 0u;
-  const uint32_t nw = (nb + 31) / 32;
-  for (uint32_t i = tid; i < nw; i += 1024) bm[i] = 0;
-  {
-    const uint32_t q = 3 + 2 * tid;
-    bool pr = (uint64_t)q * q <= limit;
-    for (uint32_t d = 3; pr && d * d <= q; d += 2)
-      if (q % d == 0) pr = false;
-    s_isp[tid] = pr ? 1 : 0;
-  }
-  __syncthreads();
-  for (uint32_t t = 0; t < 1024; ++t) {
-    const uint32_t q = 3 + 2 * t;
-    if ((uint64_t)q * q > limit) break;
-    if (!s_isp[t]) continue;
-    for (uint64_t v = (uint64_t)q * q + 2ull * q * tid; v <= limit; v += 2ull * q * 1024) {
-      const uint32_t g = (uint32_t)((v - 3) >> 1);
-      __hip_atomic_fetch_or(&bm[g >> 5], 1u << (g & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-  }
-  __syncthreads();
-  // ordered compaction: thread t owns words [t*wpt, (t+1)*wpt)
-  const uint32_t wpt = (nw + 1023) / 1024;
-  const uint32_t wb = tid * wpt, we = min(nw, wb + wpt);
-  uint32_t cnt = 0;
-  for (uint32_t w = wb; w < we; ++w) {
-    uint32_t v = ~bm[w];
-    if (w == nw - 1 && (nb & 31)) v &= (1u << (nb & 31)) - 1;
-    cnt += __popc(v);
-  }
-  s_scan[tid] = cnt;
-  __syncthreads();
-  for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive Hillis-Steele scan
-    uint32_t x = tid >= o ? s_scan[tid - o] : 0;
-    __syncthreads();
-    s_scan[tid] += x;
-    __syncthreads();
-  }
-  const uint32_t total = s_scan[1023];
-  uint32_t pos = s_scan[tid] - cnt;
-  uint32_t* Pout = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + 16);
-  uint64_t* Mout = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(table) + table_m_offset(cap));
-  if (total <= cap) {
-    for (uint32_t w = wb; w < we; ++w) {
-      uint32_t v = ~bm[w];
-      if (w == nw - 1 && (nb & 31)) v &= (1u << (nb & 31)) - 1;
-      while (v) {
-        const uint32_t b = __ffs(v) - 1;
-        v &= v - 1;
-        const uint32_t p = 3 + 2 * (w * 32 + b);
-        Pout[pos] = p;
-        Mout[pos] = ~0ull / p;
-        ++pos;
-      }
-    }
-  }
-  if (tid == 0) {
-    TableHeader* h = reinterpret_cast<TableHeader*>(table);
-    h->count = total <= cap ? total : 0xFFFFFFFFu;
-    h->cap = cap;
-    h->limit = limit;
-  }
-}
-
-
-// ---------------------------------------------------------------------------
 // Big base-prime tables (limit above kBaseLimitMax, e.g. 1e9 for the 1e18
 // window): sieve [3, limit] with the segment kernel itself, then compact the
 // prime bits into an ordered table. Scratch lives in the table's m[] region,
 // which is only written at the very end.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kCompactWordsPerThread = 8;
+constexpr uint32_t kCompactWordsPerThread = 2;
 constexpr uint32_t kCompactThreads = 256;
-constexpr uint32_t kCompactBlockWords = kCompactWordsPerThread * kCompactThreads;  // 2048 words
+constexpr uint32_t kCompactBlockWords = kCompactWordsPerThread * kCompactThreads;  // 512 words
 
 __global__ __launch_bounds__(kCompactThreads) void compact_count_kernel(const uint64_t* __restrict__ mask,
                                                                         uint64_t words,
@@ -667,23 +594,82 @@ __global__ __launch_bounds__(kCompactThreads) void compact_write_kernel(const ui
   }
 }
 
-__global__ void barrett_kernel(const void* __restrict__ table, uint64_t* __restrict__ M) {
-  const TableHeader* h = reinterpret_cast<const TableHeader*>(table);
-  const uint32_t n = h->count == 0xFFFFFFFFu ? 0u : h->count;
-  const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-    M[i] = ~0ull / P[i];
+// ---------------------------------------------------------------------------
+// Base primes up to kBaseLimitMax: many workgroups each sieve a slice of the
+// odd values 3..limit in LDS by the odd primes q <= sqrt(limit) (each
+// workgroup finds them by trial division: q <= 1568) and write the slice as
+// prime bits; the ordered compaction above then builds p[].
+// ---------------------------------------------------------------------------
+constexpr uint32_t kBaseMaskThreads = 256;
+constexpr uint32_t kBaseMaskMaxWords = 128;  // u64 words per workgroup slice
+
+__global__ __launch_bounds__(kBaseMaskThreads) void base_mask_kernel(uint64_t limit, uint64_t* __restrict__ mask,
+                                                                     uint32_t words, uint32_t wpw) {
+  __shared__ uint32_t bm[2 * kBaseMaskMaxWords];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nb = (uint32_t)((limit - 3) / 2 + 1);  // odd values 3..limit
+  const uint32_t w0 = blockIdx.x * wpw;
+  const uint32_t nw = min(wpw, words - w0);
+  for (uint32_t i = tid; i < 2 * nw; i += kBaseMaskThreads) bm[i] = 0;
+  __syncthreads();
+  const uint32_t g_lo = 64 * w0, g_hi = min(64 * (w0 + nw), nb);  // odd indices of this slice
+  for (uint32_t t = tid;; t += kBaseMaskThreads) {
+    const uint32_t q = 3 + 2 * t;
+    if ((uint64_t)q * q > limit) break;
+    bool pr = true;
+    for (uint32_t d = 3; d * d <= q; d += 2)
+      if (q % d == 0) { pr = false; break; }
+    if (!pr) continue;
+    // odd multiples v = q*m >= max(q^2, 3 + 2 g_lo): index (v - 3)/2, stride q
+    const uint64_t vlo = 3 + 2ull * g_lo;
+    uint64_t v = (uint64_t)q * q;
+    if (v < vlo) {
+      v = (vlo + q - 1) / q * q;
+      if (!(v & 1)) v += q;
+    }
+    for (uint32_t g = (uint32_t)((v - 3) >> 1); g < g_hi; g += q) {
+      const uint32_t r = g - g_lo;
+      atomicOr(&bm[r >> 5], 1u << (r & 31));
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < nw; i += kBaseMaskThreads) {
+    uint64_t v = ~((uint64_t)bm[2 * i] | ((uint64_t)bm[2 * i + 1] << 32));
+    const uint32_t gb = 64 * (w0 + i);
+    if (gb + 64 > nb) v = gb >= nb ? 0 : v & ((1ull << (nb - gb)) - 1);
+    mask[w0 + i] = v;
+  }
 }
 
 }  // namespace
 
 hipError_t launch_base_primes(uint64_t limit, void* table, uint32_t cap, hipStream_t stream) {
   if (limit > kBaseLimitMax) return hipErrorInvalidValue;
-  if (limit > 2ull * 32ull * kBaseWords + 1ull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(base_primes_kernel, dim3(1), dim3(1024), 0, stream, limit, table, cap);
+  if (limit < 3) {  // no odd primes: empty table
+    TableHeader h{0, cap, limit};
+    return hipMemcpyAsync(table, &h, sizeof(h), hipMemcpyHostToDevice, stream);
+  }
+  // scratch carved from the table's m[]/a[] region (written last): [mask][block sums]
+  char* mreg = reinterpret_cast<char*>(table) + table_m_offset(cap);
+  const uint64_t nb = (limit - 3) / 2 + 1;
+  const uint32_t words = (uint32_t)((nb + 63) / 64);
+  uint64_t* mask = reinterpret_cast<uint64_t*>(mreg);
+  const uint32_t nblocks = (words + kCompactBlockWords - 1) / kCompactBlockWords;
+  uint32_t* sums = reinterpret_cast<uint32_t*>(mreg + ((words * 8ull + 255) & ~255ull));
+  if ((uint64_t)(reinterpret_cast<char*>(sums + nblocks) - mreg) > 40ull * cap) return hipErrorInvalidValue;
+  const uint32_t wpw = std::max<uint32_t>((words + 255) / 256, 1u);
+  if (wpw > kBaseMaskMaxWords) return hipErrorInvalidValue;
+  const uint32_t grid = (words + wpw - 1) / wpw;
+  hipLaunchKernelGGL(base_mask_kernel, dim3(grid), dim3(kBaseMaskThreads), 0, stream, limit, mask, words, wpw);
+  hipLaunchKernelGGL(compact_count_kernel, dim3(nblocks), dim3(kCompactThreads), 0, stream, mask, (uint64_t)words,
+                     sums);
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(1024), 0, stream, sums, nblocks, table, cap, limit);
+  uint32_t* P = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + 16);
+  hipLaunchKernelGGL(compact_write_kernel, dim3(nblocks), dim3(kCompactThreads), 0, stream, mask, (uint64_t)words,
+                     sums, P, cap);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return launch_wheel_offsets(table, 64, stream);
+  return launch_wheel_offsets(table, 256, stream);  // m[] and a[]
 }
 
 
@@ -718,10 +704,8 @@ hipError_t launch_base_primes_big(uint64_t limit, void* table, uint32_t cap, int
   uint32_t* P = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + 16);
   hipLaunchKernelGGL(compact_write_kernel, dim3(nblocks), dim3(kCompactThreads), 0, stream, mask, words, sums, P,
                      cap);
-  hipLaunchKernelGGL(barrett_kernel, dim3(4 * (uint32_t)num_cus), dim3(256), 0, stream, table,
-                     reinterpret_cast<uint64_t*>(mreg));
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  return launch_wheel_offsets(table, num_cus, stream);
+  return launch_wheel_offsets(table, num_cus, stream);  // m[] and a[]
 }
 
 hipError_t launch_sieve_range_odd(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,

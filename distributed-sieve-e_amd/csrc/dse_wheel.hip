@@ -378,27 +378,34 @@ __device__ __forceinline__ void mark_plane(uint32_t pb32, uint32_t kk) {
 // absolute residue (q + L) & 7 (a half-wave spreads over all 8 planes). The
 // per-plane hit count is at most ceil(KP / pmin): units whose primes all
 // exceed KP (resp. KP/2) take one (two) predicated marks per plane, no loop.
+// Per-segment, per-lane constants of the L units: at step q the lane handles
+// absolute residue (q + i) & 7, whose plane byte base (pb) and -e (ne) are
+// the same for every unit of the segment.
+struct PlaneSteps {
+  uint32_t pb[8];
+  uint32_t ne[8];
+};
+
 __device__ __forceinline__ void unit_L(uint32_t* __restrict__ seg, const LargeOps& o, uint64_t Vs, uint64_t Vend,
-                                       uint64_t Kb, uint32_t pl_rot, uint32_t e_rot, uint64_t rho_pack) {
+                                       uint64_t Kb, const PlaneSteps& ps, uint32_t pl_rot, uint64_t rho_pack) {
   const uint32_t p = o.p;
   const uint64_t p2 = (uint64_t)p * p;
   const bool live = p2 < Vend;
   const bool slow = p2 > Vs;
-  const uint32_t Kbm = mod_barrett(Kb, p, o.m);
-  const uint32_t Kbm1 = Kbm + 1;
+  const uint32_t nKbm = 0u - mod_barrett(Kb, p, o.m);
   const float invp = fast_rcp((float)p);
   const uint32_t pmin = __builtin_amdgcn_readfirstlane(p);
   const uint32_t pmax = __builtin_amdgcn_readlane(p, 63);
   const bool none = __builtin_amdgcn_ballot_w64(!live || slow) != 0;
   const uint32_t n_min = (none || pmax >= KP) ? 0u : div_small(KP - pmax, pmax, fast_rcp((float)pmax));
   const uint32_t D = slow && live ? (uint32_t)(p2 - Vs) : 0u;
-  const uint32_t lds0 = lds_addr(seg);
+  if (!live) return;
 #pragma unroll
   for (uint32_t q = 0; q < 8; ++q) {
-    const uint32_t pl = (pl_rot >> (3 * q)) & 7u;
-    const uint32_t t = o.a[q] - (((e_rot >> q) & 1u) ? Kbm1 : Kbm);
-    uint32_t kk = min(t, t + p);  // (a - Kb - e) mod p
+    const uint32_t t = o.a[q] + nKbm + ps.ne[q];
+    uint32_t kk = min(t, t + p);  // plane start (a - Kb - e) mod p
     if (slow) {
+      const uint32_t pl = (pl_rot >> (3 * q)) & 7u;
       const uint32_t rho = (uint32_t)(rho_pack >> (5 * pl)) & 31u;
       const uint32_t kmin = kmin_for(D, rho);
       if (kmin > kk) {
@@ -409,13 +416,13 @@ __device__ __forceinline__ void unit_L(uint32_t* __restrict__ seg, const LargeOp
         kk += qd * p;
       }
     }
-    kk = live ? kk : KP;
-    const uint32_t pb32 = lds0 + 32 * pl;
+    const uint32_t pb32 = ps.pb[q];
     if (pmin > KP) {
-      mark_plane<true>(pb32, kk);
+      if (kk < KP) mark_plane<false>(pb32, kk);
     } else if (pmin > KP / 2) {
-      mark_plane<true>(pb32, kk);
-      mark_plane<true>(pb32, kk + p);
+      if (kk < KP) mark_plane<false>(pb32, kk);
+      kk += p;
+      if (kk < KP) mark_plane<false>(pb32, kk);
     } else {
 #pragma unroll 2
       for (uint32_t h = 0; h < n_min; ++h) {
@@ -553,6 +560,12 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       // absolute residue (q + rot) & 7 at step q: its plane and e bit
       const uint32_t pl_rot = ((wa.pl_pack >> (3 * rot)) | (wa.pl_pack << (24 - 3 * rot))) & 0xFFFFFFu;
       const uint32_t e_rot = ((wa.e_iota >> rot) | (wa.e_iota << (8 - rot))) & 0xFFu;
+      PlaneSteps ps;
+#pragma unroll
+      for (uint32_t q = 0; q < 8; ++q) {
+        ps.pb[q] = lds_addr(seg) + 32 * ((pl_rot >> (3 * q)) & 7u);
+        ps.ne[q] = 0u - ((e_rot >> q) & 1u);
+      }
       const uint64_t Kb = wa.KB0 + s * (uint64_t)KP;
       LargeOps nxt;
       auto l_index = [&](uint32_t r) { return (r & 1) ? r * NW + (NW - 1 - wave) : r * NW + wave; };
@@ -578,7 +591,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
           const uint32_t un = l_index(r + 1);
           if (un < n2) load_L(nxt, P, M, A, i_mid1 + 64 * un + lane, np);  // prefetch
           const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p);
-          if ((phases & kPhaseLarge) && (uint64_t)p0 * p0 < Vend) unit_L(seg, cur, Vs, Vend, Kb, pl_rot, e_rot, wa.rho_pack);
+          if ((phases & kPhaseLarge) && (uint64_t)p0 * p0 < Vend) unit_L(seg, cur, Vs, Vend, Kb, ps, pl_rot, wa.rho_pack);
         }
       }
     }
@@ -662,21 +675,23 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   }
 }
 
-// a[8i+j] = first k >= 0 with p | R30[j] + 30k, for every table prime >= 7.
+// m[i] = floor((2^64-1)/p) and the rotated wheel-offset row of every table
+// prime: a[8i + ((j - i) & 7)] = first k >= 0 with p | R30[j] + 30k (p >= 7).
 __global__ void wheel_offsets_kernel(void* __restrict__ table) {
   const TableHeader* h = reinterpret_cast<const TableHeader*>(table);
   const uint32_t n = h->count == 0xFFFFFFFFu ? 0u : h->count;
   const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
-  const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(h->cap));
+  uint64_t* M = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(table) + table_m_offset(h->cap));
   uint32_t* A = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + table_a_offset(h->cap));
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t p = P[i];
+    const uint64_t m = ~0ull / p;
+    M[i] = m;
     if (p < 7) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) A[8ull * i + j] = 0;
       continue;
     }
-    const uint64_t m = M[i];
     const uint64_t inv = inv30_of(p);
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
