@@ -37,7 +37,7 @@ constexpr uint32_t kR30[8] = {1, 7, 11, 13, 17, 19, 23, 29};
 constexpr int kWheelLogKP = 17;
 constexpr uint64_t kWheelSpan = 30ull << kWheelLogKP;   // integers per segment
 constexpr uint64_t kWheelOutBits = kWheelSpan / 2;      // odd candidates per segment
-// Largest base prime the wheel kernel takes (above: odd-only kernel for now).
+// Base primes above this go through the bucketed pass (dse_wheel.hip).
 constexpr uint64_t kWheelMaxPrime = 1ull << 21;
 
 // Segment geometry of the marking kernel (see DESIGN.md "Kernels").

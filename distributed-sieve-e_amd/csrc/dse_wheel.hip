@@ -37,6 +37,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "dse_internal.h"
 
 namespace dse {
@@ -94,6 +96,8 @@ struct WheelArgs {
   uint32_t fix0;       // output word 0 bits of the primes 3..61 inside the range
   uint32_t phases;
   uint8_t v0q[kNQ];    // V0 mod q
+  const uint32_t* bk_entries;  // bucketed hits of the primes > kWheelMaxPrime (or null):
+  const uint32_t* bk_start;    // segment s owns entries [bk_start[s], bk_start[s+1]), k | plane << 17
 };
 
 __device__ __forceinline__ void lds_or(uint32_t* a, uint32_t v) {
@@ -447,7 +451,7 @@ struct WheelLds {
   uint64_t mid_m[kMidCap];         // Barrett factors of the staged mid primes
   uint32_t mid_p[kMidCap];         // p | (30^{-1} mod p) << 16
   uint32_t lut[256];               // period byte -> 15 odd slots
-  uint32_t thr[3];
+  uint32_t thr[4];
   unsigned long long wave_cnt[NW];
 };
 
@@ -486,6 +490,10 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     hi = np;
     while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= TB) lo = mid + 1; else hi = mid; }
     s_thr[2] = min(lo, s_thr[0] + kMidCap);
+    lo = s_thr[2];
+    hi = np;  // primes above kWheelMaxPrime are bucketed (or absent)
+    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= kWheelMaxPrime) lo = mid + 1; else hi = mid; }
+    s_thr[3] = lo;
   }
   if (tid < 256) {
     uint32_t v = 0;
@@ -511,7 +519,8 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   const uint32_t nA = i_midB - i_mid0;
   const uint32_t n_mid = i_mid1 - i_mid0;
   const uint32_t nB = (i_mid1 - i_midB + 7) / 8;
-  const uint32_t nL = (np - i_mid1 + 63) / 64;
+  const uint32_t i_big = s_thr[3];             // L units end here
+  const uint32_t nL = (i_big - i_mid1 + 63) / 64;
   const uint32_t n1 = nA + nB, n2 = nL;
   // Issue arbitration favours older waves: on equal static shares the four
   // youngest waves finish the mark phase ~17% after the rest (measured with a
@@ -589,7 +598,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         const uint32_t b = NW * R_cut + (r - R_cut) * kSkewWaves;
         return (r & 1) ? b + (kSkewWaves - 1 - wave) : b + wave;
       };
-      if (l_index(0) < n2) load_L(nxt, P, M, A, i_mid1 + 64 * l_index(0) + lane, np);
+      if (l_index(0) < n2) load_L(nxt, P, M, A, i_mid1 + 64 * l_index(0) + lane, i_big);
       for (uint32_t r = 0; r < n_rounds; ++r) {
         const uint32_t u = l_index(r);
         if (u < n1) {
@@ -609,9 +618,18 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         if (u < n2) {
           const LargeOps cur = nxt;
           const uint32_t un = l_index(r + 1);
-          if (un < n2) load_L(nxt, P, M, A, i_mid1 + 64 * un + lane, np);  // prefetch
+          if (un < n2) load_L(nxt, P, M, A, i_mid1 + 64 * un + lane, i_big);  // prefetch
           const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p);
           if ((phases & kPhaseLarge) && (uint64_t)p0 * p0 < Vend) unit_L(seg, cur, Vs, Vend, Kb, ps, pl_rot, wa.rho_pack);
+        }
+      }
+      // bucketed hits of the primes > kWheelMaxPrime: one entry per thread
+      if (wa.bk_start && (phases & kPhaseLarge)) {
+        const uint32_t b0 = wa.bk_start[s], b1 = wa.bk_start[s + 1];
+        const uint32_t lds0 = lds_addr(seg);
+        for (uint32_t j = b0 + tid; j < b1; j += NT) {
+          const uint32_t e = wa.bk_entries[j];
+          mark_plane<false>(lds0 + 32 * (e >> 17), e & (KP - 1));
         }
       }
     }
@@ -722,6 +740,143 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Bucketed pass for the primes above kWheelMaxPrime (high-offset windows):
+// such a prime hits a 3.9 M-integer segment less than once, so instead of
+// visiting every (prime, segment) pair the kernels below walk each prime's
+// multiples p*m, gcd(m, 30) = 1, across the whole range once and file every
+// hit under its segment: k | plane << 17. Two identical walks: count (LDS
+// per-segment counters -> per-workgroup column), then fill (LDS cursors
+// seeded from the scanned columns). The wheel kernel ORs its segment's list.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kBucketThreads = 256;
+constexpr uint32_t kBucketGrid = 1024;           // workgroups of the count / fill walks
+constexpr uint32_t kBucketMaxSegs = 8192;        // segments per pass (LDS counters)
+constexpr uint32_t kCoprime30 = (1u << 1) | (1u << 7) | (1u << 11) | (1u << 13) | (1u << 17) | (1u << 19) |
+                                (1u << 23) | (1u << 29);
+// gap from R30[w] to the next coprime residue: 6 4 2 4 2 4 6 2 (3 bits each)
+constexpr uint32_t kGap30 = 6u | (4u << 3) | (2u << 6) | (4u << 9) | (2u << 12) | (4u << 15) | (6u << 18) | (2u << 21);
+
+struct BucketArgs {
+  uint64_t V0;         // v_start - 1 of the pass
+  uint64_t span;       // integers covered by the pass: nseg * kWheelSpan
+  uint64_t plane_lut;  // plane of relative residue rho (odd) in bits [3(rho >> 1), +3)
+  uint32_t nseg;       // segments in the pass (<= kBucketMaxSegs)
+  uint64_t vmax;       // largest value of the pass (primes with p^2 > vmax have no hits)
+};
+
+// i_lo = first table index with p > kWheelMaxPrime, i_hi = first with p^2 > vmax
+__global__ void bucket_range_kernel(const void* __restrict__ table, uint64_t vmax, uint32_t* __restrict__ range) {
+  const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
+  const uint32_t np = th->count == 0xFFFFFFFFu ? 0u : th->count;
+  const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
+  uint32_t lo = 0, hi = np;
+  while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= kWheelMaxPrime) lo = mid + 1; else hi = mid; }
+  range[0] = lo;
+  hi = np;
+  while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if ((uint64_t)P[mid] * P[mid] <= vmax) lo = mid + 1; else hi = mid; }
+  range[1] = lo;
+}
+
+// Walk the coprime-to-30 multiples of p inside [V0 + 1, V0 + span), from p^2 on.
+template <typename Emit>
+__device__ __forceinline__ void bucket_walk(uint32_t p, uint64_t m, const BucketArgs& ba, Emit emit) {
+  const uint64_t p2 = (uint64_t)p * p;
+  const uint64_t vlo = max(ba.V0 + 1, p2);
+  uint64_t q = __umul64hi(vlo, m);  // floor(vlo / p), corrected
+  uint64_t r = vlo - q * p;
+  while (r >= p) { r -= p; ++q; }
+  const uint64_t m0 = q + (r != 0);
+  const uint32_t r30 = (uint32_t)(m0 % 30);
+  const uint32_t d = __builtin_ctz(kCoprime30 >> r30);
+  uint32_t w3 = 3 * __popc(kCoprime30 & ((1u << (r30 + d)) - 1));  // 3 * index of (m mod 30) in R30
+  uint64_t o = (uint64_t)p * (m0 + d) - ba.V0;
+  while (o < ba.span) {
+    const uint32_t s = ((uint32_t)(o >> 17)) / 30u;  // o < 2^49
+    const uint32_t u = (uint32_t)(o - (uint64_t)s * kWheelSpan);
+    const uint32_t k = u / 30u, rho = u - 30u * k;
+    const uint32_t pl = (uint32_t)(ba.plane_lut >> (3 * (rho >> 1))) & 7u;
+    emit(s, k | (pl << 17));
+    o += (uint64_t)p * ((kGap30 >> w3) & 7u);
+    w3 = w3 == 21 ? 0u : w3 + 3;
+  }
+}
+
+__global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(const void* __restrict__ table, BucketArgs ba,
+                                                                    const uint32_t* __restrict__ range,
+                                                                    uint32_t* __restrict__ cols) {
+  __shared__ uint32_t cnt[kBucketMaxSegs];
+  const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
+  const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
+  const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
+  for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) cnt[j] = 0;
+  __syncthreads();
+  const uint32_t i_lo = range[0], i_hi = range[1];
+  for (uint32_t i = i_lo + blockIdx.x * kBucketThreads + threadIdx.x; i < i_hi; i += kBucketGrid * kBucketThreads)
+    bucket_walk(P[i], M[i], ba, [&](uint32_t sg, uint32_t) { atomicAdd(&cnt[sg], 1u); });
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) cols[(uint64_t)j * kBucketGrid + blockIdx.x] = cnt[j];
+}
+
+// per segment: exclusive scan of its column over the workgroups, in place; total -> tot[s]
+__global__ void bucket_colscan_kernel(uint32_t* __restrict__ cols, uint32_t nseg, uint32_t* __restrict__ tot) {
+  const uint32_t sg = blockIdx.x * blockDim.x + threadIdx.x;
+  if (sg >= nseg) return;
+  uint32_t* c = cols + (uint64_t)sg * kBucketGrid;
+  uint32_t run = 0;
+  for (uint32_t g = 0; g < kBucketGrid; ++g) {
+    const uint32_t v = c[g];
+    c[g] = run;
+    run += v;
+  }
+  tot[sg] = run;
+}
+
+// exclusive scan of the segment totals -> start[0..nseg]
+__global__ __launch_bounds__(1024) void bucket_startscan_kernel(const uint32_t* __restrict__ tot, uint32_t nseg,
+                                                                uint32_t* __restrict__ start) {
+  __shared__ uint32_t s_scan[1024];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t per = (nseg + 1023) / 1024;
+  const uint32_t b0 = tid * per, b1 = min(nseg, b0 + per);
+  uint32_t sum = 0;
+  for (uint32_t b = b0; b < b1; ++b) sum += tot[b];
+  s_scan[tid] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < 1024; o <<= 1) {
+    const uint32_t x = tid >= o ? s_scan[tid - o] : 0;
+    __syncthreads();
+    s_scan[tid] += x;
+    __syncthreads();
+  }
+  uint32_t run = s_scan[tid] - sum;
+  for (uint32_t b = b0; b < b1; ++b) {
+    start[b] = run;
+    run += tot[b];
+  }
+  if (tid == 1023) start[nseg] = s_scan[1023];
+}
+
+__global__ __launch_bounds__(kBucketThreads) void bucket_fill_kernel(const void* __restrict__ table, BucketArgs ba,
+                                                                   const uint32_t* __restrict__ range,
+                                                                   const uint32_t* __restrict__ cols,
+                                                                   const uint32_t* __restrict__ start,
+                                                                   uint32_t* __restrict__ entries, uint64_t cap) {
+  __shared__ uint32_t cur[kBucketMaxSegs];
+  const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
+  const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
+  const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
+  for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads)
+    cur[j] = start[j] + cols[(uint64_t)j * kBucketGrid + blockIdx.x];
+  __syncthreads();
+  const uint32_t i_lo = range[0], i_hi = range[1];
+  for (uint32_t i = i_lo + blockIdx.x * kBucketThreads + threadIdx.x; i < i_hi; i += kBucketGrid * kBucketThreads)
+    bucket_walk(P[i], M[i], ba, [&](uint32_t sg, uint32_t e) {
+      const uint32_t pos = atomicAdd(&cur[sg], 1u);
+      if (pos < cap) entries[pos] = e;
+    });
+}
+
 }  // namespace
 
 hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream) {
@@ -729,9 +884,10 @@ hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream) {
   return hipGetLastError();
 }
 
-hipError_t launch_sieve_range_wheel(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
-                                    unsigned long long* count, int num_cus, hipStream_t stream) {
-  if (nbits == 0) return hipSuccess;
+namespace {
+
+// Launch geometry shared by the wheel kernel and the bucket walks.
+WheelArgs make_wheel_args(uint64_t g_start, uint64_t nbits, uint64_t* plane_lut) {
   static const uint32_t phases = [] {
     const char* e = getenv("DSE_PHASES");  // profiling-only ablation knob
     return e ? (uint32_t)strtoul(e, nullptr, 0) & kPhaseAll : kPhaseAll;
@@ -743,6 +899,7 @@ hipError_t launch_sieve_range_wheel(const void* table, uint64_t g_start, uint64_
   wa.KB0 = wa.V0 / 30;
   const uint32_t v0m = (uint32_t)(wa.V0 % 30);
   uint32_t n = 0;
+  *plane_lut = 0;
   for (uint32_t rho = 1; rho < 30; rho += 2) {
     const uint32_t r = (v0m + rho) % 30;
     if (r % 3 == 0 || r % 5 == 0) continue;
@@ -751,38 +908,138 @@ hipError_t launch_sieve_range_wheel(const void* table, uint64_t g_start, uint64_
     wa.rho_pack |= (uint64_t)rho << (5 * n);
     wa.pl_pack |= n << (3 * iota);
     if (v0m + rho >= 30) wa.e_iota |= 1u << iota;
+    *plane_lut |= (uint64_t)n << (3 * (rho >> 1));
     ++n;
   }
-  if (n != 8) return hipErrorInvalidValue;
   // primes 3..61 inside the range: the wheel drops 3 and 5, the patterns mark 7..61 themselves
   constexpr uint32_t small[] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61};
   for (uint32_t v : small)
     if (v >= v_start && (v - v_start) / 2 < nbits) wa.fix0 |= 1u << ((v - v_start) / 2);
   for (int j = 0; j < kNQ; ++j) wa.v0q[j] = (uint8_t)(wa.V0 % kQ[j]);
   wa.phases = phases;
-  const uint64_t nseg = (nbits + kWheelOutBits - 1) / kWheelOutBits;
+  return wa;
+}
+
+uint64_t isqrt64(uint64_t x) {
+  uint64_t r = (uint64_t)__builtin_sqrt((double)x);
+  while (r * r > x) --r;
+  while ((r + 1) * (r + 1) <= x) ++r;
+  return r;
+}
+
+// Rigorous bound on the bucket entries of a pass spanning `span` integers with
+// primes in (a, b]: each prime has <= 8 span / (30 p) + 8 coprime multiples;
+// sum 1/p <= ln(ln b / ln a) + 1/ln^2 a and pi(b) <= 1.25506 b / ln b.
+uint64_t bucket_cap(uint64_t span, double a, double b) {
+  if (b <= a) return 64;
+  const double la = __builtin_log(a), lb = __builtin_log(b);
+  const double s = __builtin_log(lb / la) + 1.0 / (la * la);
+  return (uint64_t)(8.0 * (double)span / 30.0 * s + 8.0 * 1.25506 * b / lb) + 1024;
+}
+
+constexpr uint64_t kBucketMaxEntries = 1ull << 31;  // 8 GB of entries per pass
+
+// Per-device scratch for the bucket pass (grow-only; freed with the process).
+struct Scratch {
+  void* ptr = nullptr;
+  uint64_t bytes = 0;
+};
+Scratch g_scratch[64];
+
+hipError_t bucket_scratch(uint64_t bytes, char** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  Scratch& sc = g_scratch[dev];
+  if (sc.bytes < bytes) {
+    if (sc.ptr && (e = hipFree(sc.ptr)) != hipSuccess) return e;
+    sc.ptr = nullptr;
+    sc.bytes = 0;
+    if ((e = hipMalloc(&sc.ptr, bytes)) != hipSuccess) return e;
+    sc.bytes = bytes;
+  }
+  *out = static_cast<char*>(sc.ptr);
+  return hipSuccess;
+}
+
+hipError_t launch_wheel(const void* table, const WheelArgs& wa, uint32_t* out, unsigned long long* count,
+                        int num_cus, hipStream_t stream) {
+  const uint64_t nseg = (wa.nbits + kWheelOutBits - 1) / kWheelOutBits;
   const uint64_t grid = nseg < (uint64_t)num_cus ? nseg : (uint64_t)num_cus;
   hipLaunchKernelGGL(wheel_segments_kernel, dim3((uint32_t)grid), dim3(NT), 0, stream, table, wa, out, count);
   return hipGetLastError();
 }
 
-// Kernel choice: the wheel kernel for base primes up to kWheelMaxPrime (every
-// configured N up to 4.4e12), the odd-only kernel above (high-offset windows).
+}  // namespace
+
+hipError_t launch_sieve_range_wheel(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
+                                    unsigned long long* count, int num_cus, hipStream_t stream) {
+  if (nbits == 0) return hipSuccess;
+  const uint64_t vmax = 3 + 2 * (g_start + nbits - 1);
+  const uint64_t root = isqrt64(vmax);
+  uint64_t plane_lut;
+  if (root <= kWheelMaxPrime) {
+    const WheelArgs wa = make_wheel_args(g_start, nbits, &plane_lut);
+    return launch_wheel(table, wa, out, count, num_cus, stream);
+  }
+  // primes above kWheelMaxPrime: passes of <= kBucketMaxSegs segments, each
+  // with its own bucket build, then the wheel kernel over the pass
+  const uint64_t total_seg = (nbits + kWheelOutBits - 1) / kWheelOutBits;
+  for (uint64_t s0 = 0; s0 < total_seg;) {
+    uint64_t ns = std::min<uint64_t>(kBucketMaxSegs, total_seg - s0);
+    while (ns > 1 && bucket_cap(ns * kWheelSpan, (double)kWheelMaxPrime, (double)root) > kBucketMaxEntries) ns /= 2;
+    const uint64_t g0 = g_start + s0 * kWheelOutBits;
+    const uint64_t nb = std::min<uint64_t>(nbits - s0 * kWheelOutBits, ns * kWheelOutBits);
+    const uint64_t vmax_p = 3 + 2 * (g0 + nb - 1);
+    WheelArgs wa = make_wheel_args(g0, nb, &plane_lut);
+    BucketArgs ba{};
+    ba.V0 = wa.V0;
+    ba.span = ns * kWheelSpan;
+    ba.plane_lut = plane_lut;
+    ba.nseg = (uint32_t)ns;
+    ba.vmax = vmax_p;
+    const uint64_t cap = bucket_cap(ba.span, (double)kWheelMaxPrime, (double)isqrt64(vmax_p));
+    // scratch: [range 2][cols grid*ns][tot ns][start ns+1][entries cap]
+    const uint64_t o_cols = 256, o_tot = o_cols + 4ull * kBucketGrid * ns, o_start = o_tot + 4 * ns + 256,
+                   o_ent = (o_start + 4 * (ns + 1) + 255) & ~255ull, bytes = o_ent + 4 * cap;
+    char* sc = nullptr;
+    hipError_t e = bucket_scratch(bytes, &sc);
+    if (e != hipSuccess) return e;
+    uint32_t* range = reinterpret_cast<uint32_t*>(sc);
+    uint32_t* cols = reinterpret_cast<uint32_t*>(sc + o_cols);
+    uint32_t* tot = reinterpret_cast<uint32_t*>(sc + o_tot);
+    uint32_t* start = reinterpret_cast<uint32_t*>(sc + o_start);
+    uint32_t* ent = reinterpret_cast<uint32_t*>(sc + o_ent);
+    hipLaunchKernelGGL(bucket_range_kernel, dim3(1), dim3(1), 0, stream, table, vmax_p, range);
+    hipLaunchKernelGGL(bucket_count_kernel, dim3(kBucketGrid), dim3(kBucketThreads), 0, stream, table, ba, range, cols);
+    hipLaunchKernelGGL(bucket_colscan_kernel, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, stream, cols,
+                       (uint32_t)ns, tot);
+    hipLaunchKernelGGL(bucket_startscan_kernel, dim3(1), dim3(1024), 0, stream, tot, (uint32_t)ns, start);
+    hipLaunchKernelGGL(bucket_fill_kernel, dim3(kBucketGrid), dim3(kBucketThreads), 0, stream, table, ba, range, cols,
+                       start, ent, cap);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    wa.bk_entries = ent;
+    wa.bk_start = start;
+    if ((e = launch_wheel(table, wa, out ? out + s0 * (kWheelOutBits / 32) : nullptr, count, num_cus, stream)) !=
+        hipSuccess)
+      return e;
+    s0 += ns;
+  }
+  return hipSuccess;
+}
+
+// Kernel choice: the wheel kernel (with the bucketed pass above
+// kWheelMaxPrime); DSE_KERNEL=odd forces the round-1 odd-only kernel (A/B).
 hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
                               unsigned long long* count, int num_cus, hipStream_t stream) {
   if (nbits == 0) return hipSuccess;
-  static const int force = [] {
-    const char* e = getenv("DSE_KERNEL");  // profiling-only: "odd" or "wheel"
-    if (!e) return 0;
-    return e[0] == 'o' ? 1 : e[0] == 'w' ? 2 : 0;
+  static const bool odd = [] {
+    const char* e = getenv("DSE_KERNEL");  // profiling-only
+    return e && e[0] == 'o';
   }();
-  const uint64_t vmax = 3 + 2 * (g_start + nbits - 1);
-  uint64_t r = (uint64_t)__builtin_sqrt((double)vmax);
-  while (r * r > vmax) --r;
-  while ((r + 1) * (r + 1) <= vmax) ++r;
-  const bool wheel = force ? force == 2 : r <= kWheelMaxPrime;
-  return wheel ? launch_sieve_range_wheel(table, g_start, nbits, out, count, num_cus, stream)
-               : launch_sieve_range_odd(table, g_start, nbits, out, count, num_cus, stream);
+  return odd ? launch_sieve_range_odd(table, g_start, nbits, out, count, num_cus, stream)
+             : launch_sieve_range_wheel(table, g_start, nbits, out, count, num_cus, stream);
 }
 
 }  // namespace dse
