@@ -750,8 +750,14 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
 // seeded from the scanned columns). The wheel kernel ORs its segment's list.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kBucketThreads = 256;
-constexpr uint32_t kBucketGrid = 1024;           // workgroups of the count / fill walks
-constexpr uint32_t kBucketMaxSegs = 8192;        // segments per pass (LDS counters)
+#ifndef DSE_BK_GRID
+#define DSE_BK_GRID 1024
+#endif
+#ifndef DSE_BK_SEGS
+#define DSE_BK_SEGS 8192
+#endif
+constexpr uint32_t kBucketGrid = DSE_BK_GRID;    // workgroups of the count / fill walks
+constexpr uint32_t kBucketMaxSegs = DSE_BK_SEGS; // segments per pass (LDS counters)
 constexpr uint32_t kCoprime30 = (1u << 1) | (1u << 7) | (1u << 11) | (1u << 13) | (1u << 17) | (1u << 19) |
                                 (1u << 23) | (1u << 29);
 // gap from R30[w] to the next coprime residue: 6 4 2 4 2 4 6 2 (3 bits each)
@@ -986,8 +992,13 @@ hipError_t launch_sieve_range_wheel(const void* table, uint64_t g_start, uint64_
   // primes above kWheelMaxPrime: passes of <= kBucketMaxSegs segments, each
   // with its own bucket build, then the wheel kernel over the pass
   const uint64_t total_seg = (nbits + kWheelOutBits - 1) / kWheelOutBits;
+  uint64_t max_segs = kBucketMaxSegs;
+  if (const char* e = getenv("DSE_BUCKET_PASS_SEGS")) {  // test-only: force small passes
+    const uint64_t v = strtoull(e, nullptr, 0);
+    if (v >= 1 && v < max_segs) max_segs = v;
+  }
   for (uint64_t s0 = 0; s0 < total_seg;) {
-    uint64_t ns = std::min<uint64_t>(kBucketMaxSegs, total_seg - s0);
+    uint64_t ns = std::min<uint64_t>(max_segs, total_seg - s0);
     while (ns > 1 && bucket_cap(ns * kWheelSpan, (double)kWheelMaxPrime, (double)root) > kBucketMaxEntries) ns /= 2;
     const uint64_t g0 = g_start + s0 * kWheelOutBits;
     const uint64_t nb = std::min<uint64_t>(nbits - s0 * kWheelOutBits, ns * kWheelOutBits);

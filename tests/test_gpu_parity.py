@@ -259,3 +259,23 @@ def test_window_1e18_full(ctx):
     total = ctx.sieve_window(10**18, 10**18 + 10**10)
     parts = sum(ctx.sieve_window(10**18 + k * 10**9 + (1 if k else 0), 10**18 + (k + 1) * 10**9) for k in range(10))
     assert total == parts == 241_272_176
+
+
+# ---- bucketed pass (primes > 2^21) ----
+
+def test_bucket_threshold_window_vs_oracle(ctx, oracle):
+    """1e13: base primes up to 3.16e6, the ones above 2^21 go through buckets."""
+    g0, nb = (10**13 + 1 - 3) // 2, 5 * 10**7
+    m, c = ctx.sieve_odd_range(g0, nb)
+    m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
+    assert c == c_ref and np.array_equal(m, m_ref)
+
+
+def test_bucket_multi_pass_mask(ctx, oracle, monkeypatch):
+    """Passes of 3 segments (DSE_BUCKET_PASS_SEGS, test-only knob): the pass
+    boundaries, the per-pass bucket builds and the output offsets, bit-exact."""
+    monkeypatch.setenv("DSE_BUCKET_PASS_SEGS", "3")
+    g0, nb = (10**14 + 12345) // 2 * 1 + 7, 10 * 1966080 + 12345  # ragged start and end, 11 segments
+    m, c = ctx.sieve_odd_range(g0, nb)
+    m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
+    assert c == c_ref and np.array_equal(m, m_ref)
