@@ -60,14 +60,6 @@ constexpr uint32_t TA = LS / 16;            // A/B threshold
 #endif
 constexpr uint32_t TB = DSE_TB;             // B/L threshold (<= LS)
 static_assert(TB <= LS && TB >= TA, "B/L threshold");
-#ifndef DSE_SKEW_WAVES
-#define DSE_SKEW_WAVES 12
-#endif
-#ifndef DSE_SKEW_DIV
-#define DSE_SKEW_DIV 3
-#endif
-constexpr uint32_t kSkewWaves = DSE_SKEW_WAVES;  // waves that take the rounds from R_cut on
-constexpr uint32_t kSkewDiv = DSE_SKEW_DIV;      // R_cut = R_full - R_full / kSkewDiv
 constexpr uint32_t kMidCap = TB >= 16384 ? 1920 : TB >= 8192 ? 1040 : TB >= 4096 ? 580 : 320;  // odd primes in (61, TB]
 constexpr uint32_t kOutWordsPerSeg = (uint32_t)(kWheelOutBits / 32);  // 61440
 
@@ -452,8 +444,24 @@ struct WheelLds {
   uint32_t mid_p[kMidCap];         // p | (30^{-1} mod p) << 16
   uint32_t lut[256];               // period byte -> 15 odd slots
   uint32_t thr[4];
+  uint32_t ctr;                    // dynamic unit counter of the current segment
   unsigned long long wave_cnt[NW];
 };
+
+#ifdef DSE_TIMING
+// Debug build only: per-wave cycle stamps at the phase boundaries of segment
+// index 5 of each workgroup -> dse_timing[block][wave][5] (tools/wave_timing.py).
+__device__ unsigned long long dse_timing[256 * 16 * 5];
+#define DSE_TSTAMP(i)                                                                          \
+  do {                                                                                         \
+    if (s == blockIdx.x + 5ull * gridDim.x && lane_id == 0 && blockIdx.x < 256)                 \
+      dse_timing[(blockIdx.x * 16 + wave) * 5 + (i)] = __builtin_readcyclecounter();            \
+  } while (0)
+#else
+#define DSE_TSTAMP(i) \
+  do {                \
+  } while (0)
+#endif
 
 __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restrict__ table, WheelArgs wa,
                                                             uint32_t* __restrict__ out,
@@ -512,24 +520,17 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     s_mid_m[i] = M[i_mid0 + i];
   }
   // Work units: list 1 = nA single mid primes, then nB diagonal units (8
-  // primes each); list 2 = nL large units (64 primes each). Round r of wave w
-  // takes unit r*16 + w (r even) or r*16 + 15 - w (r odd) of BOTH lists, so
-  // every wave gets the same mix of LDS-bound and latency-bound units and a
-  // balanced share of the sorted (cost ~ 1/p) lists. No atomics, no drains.
+  // primes each); list 2 = nL large units (64 primes each); handed out through
+  // one dynamic queue (mark phase below). Issue arbitration favours older
+  // waves, so any static split finishes the youngest waves last (1.17x the
+  // mean on equal shares, measured with DSE_TIMING); the queue makes them take
+  // fewer units instead.
   const uint32_t nA = i_midB - i_mid0;
   const uint32_t n_mid = i_mid1 - i_mid0;
   const uint32_t nB = (i_mid1 - i_midB + 7) / 8;
   const uint32_t i_big = s_thr[3];             // L units end here
   const uint32_t nL = (i_big - i_mid1 + 63) / 64;
   const uint32_t n1 = nA + nB, n2 = nL;
-  // Issue arbitration favours older waves: on equal static shares the four
-  // youngest waves finish the mark phase ~17% after the rest (measured with a
-  // DSE_TIMING build). Rounds from R_cut on are therefore spread over the
-  // kSkewWaves oldest waves only.
-  const uint32_t n_units12 = max(n1, n2);
-  const uint32_t R_full = (n_units12 + NW - 1) / NW;
-  const uint32_t R_cut = R_full - R_full / kSkewDiv;
-  const uint32_t n_rounds = R_cut + (n_units12 > NW * R_cut ? (n_units12 - NW * R_cut + kSkewWaves - 1) / kSkewWaves : 0);
 
   const uint64_t out_words = 2ull * ((wa.nbits + 63) / 64);  // 32-bit words of the caller's mask
   const uint64_t nseg = (wa.nbits + kWheelOutBits - 1) / kWheelOutBits;
@@ -543,6 +544,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     uint32_t lane = lane_id;
     asm volatile("" : "+v"(lane));
 
+    DSE_TSTAMP(0);
     // ---- 1. init: small-prime patterns (7..61) -------------------------
     {
       const uint32_t C = lane, pl = lane >> 3, c = lane & 7;
@@ -575,8 +577,10 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         seg[(r0 + r) * 64 + C] = (uint32_t)w;
         seg[(r0 + r + 1) * 64 + C] = (uint32_t)(w >> 32);
       }
+      if (tid == 0) lds.ctr = 0;
     }
     __syncthreads();
+    DSE_TSTAMP(1);
 
     // ---- 2. mark -------------------------------------------------------
     if (phases & kPhaseUnits) {
@@ -591,37 +595,47 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         ps.ne[q] = 0u - ((e_rot >> q) & 1u);
       }
       const uint64_t Kb = wa.KB0 + s * (uint64_t)KP;
-      LargeOps nxt;
-      auto l_index = [&](uint32_t r) -> uint32_t {
-        if (r < R_cut) return (r & 1) ? r * NW + (NW - 1 - wave) : r * NW + wave;
-        if (wave >= kSkewWaves) return 0xFFFFFFFFu;
-        const uint32_t b = NW * R_cut + (r - R_cut) * kSkewWaves;
-        return (r & 1) ? b + (kSkewWaves - 1 - wave) : b + wave;
+      // One dynamic queue over both lists, interleaved (list 1 at even, list 2
+      // at odd positions while both last). Claims run two units ahead: the LDS
+      // atomic for unit j+2 is issued when unit j starts and read when it ends
+      // (by then this wave's marks of unit j have drained), and a large unit's
+      // operands are loaded while the unit before it runs.
+      const uint32_t n_int = min(n1, n2), n_all = n1 + n2;
+      auto claim = [&]() -> uint32_t {
+        uint32_t j = 0;
+        if (lane == 0) j = atomicAdd(&lds.ctr, 1u);
+        return j;  // per-lane value; lane 0 holds the claim
       };
-      if (l_index(0) < n2) load_L(nxt, P, M, A, i_mid1 + 64 * l_index(0) + lane, i_big);
-      for (uint32_t r = 0; r < n_rounds; ++r) {
-        const uint32_t u = l_index(r);
-        if (u < n1) {
-          if (u < nA) {
-            const uint32_t pi = __builtin_amdgcn_readfirstlane(s_mid_p[u]);
+      auto is_l = [&](uint32_t u) -> bool { return u < 2 * n_int ? (u & 1) != 0 : n2 > n1; };
+      auto idx_of = [&](uint32_t u) -> uint32_t { return u < 2 * n_int ? u >> 1 : u - n_int; };
+      LargeOps cur, nxt;
+      uint32_t u_cur = __builtin_amdgcn_readlane(claim(), 0);
+      uint32_t u_nxt = __builtin_amdgcn_readlane(claim(), 0);
+      if (u_cur < n_all && is_l(u_cur)) load_L(cur, P, M, A, i_mid1 + 64 * idx_of(u_cur) + lane, i_big);
+      while (u_cur < n_all) {
+        const uint32_t c2 = claim();  // unit after next, read at the end of this one
+        if (u_nxt < n_all && is_l(u_nxt)) load_L(nxt, P, M, A, i_mid1 + 64 * idx_of(u_nxt) + lane, i_big);
+        const uint32_t k = idx_of(u_cur);
+        if (!is_l(u_cur)) {
+          if (k < nA) {
+            const uint32_t pi = __builtin_amdgcn_readfirstlane(s_mid_p[k]);
             const uint32_t p = pi & 0xFFFFu;
-            const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mid_m[u] >> 32)) << 32) |
-                               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_mid_m[u]);  // (int -> no sign extension)
+            const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mid_m[k] >> 32)) << 32) |
+                               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_mid_m[k]);
             if ((phases & kPhaseMidA) && (uint64_t)p * p < Vend) unit_A(seg, pi, m, Vs, wa.rho_pack, lane);
           } else {
-            const uint32_t j0 = nA + (u - nA) * 8;
+            const uint32_t j0 = nA + (k - nA) * 8;
             const uint32_t pf = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
             if ((phases & kPhaseMidB) && (uint64_t)pf * pf < Vend)
               unit_B(seg, s_mid_p, s_mid_m, j0, min(8u, n_mid - j0), Vs, Vend, wa.rho_pack, lane);
           }
-        }
-        if (u < n2) {
-          const LargeOps cur = nxt;
-          const uint32_t un = l_index(r + 1);
-          if (un < n2) load_L(nxt, P, M, A, i_mid1 + 64 * un + lane, i_big);  // prefetch
+        } else {
           const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p);
           if ((phases & kPhaseLarge) && (uint64_t)p0 * p0 < Vend) unit_L(seg, cur, Vs, Vend, Kb, ps, pl_rot, wa.rho_pack);
         }
+        cur = nxt;
+        u_cur = u_nxt;
+        u_nxt = __builtin_amdgcn_readlane(c2, 0);
       }
       // bucketed hits of the primes > kWheelMaxPrime: one entry per thread
       if (wa.bk_start && (phases & kPhaseLarge)) {
@@ -634,7 +648,9 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       }
     }
     lds_drain();
+    DSE_TSTAMP(2);
     __syncthreads();
+    DSE_TSTAMP(3);
 
     // ---- 3. expand to odd-only bits, count, store ------------------------
     if (phases & kPhaseExpand) {
@@ -700,6 +716,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       }
     }
     __syncthreads();
+    DSE_TSTAMP(4);
   }
 
 #pragma unroll
@@ -889,6 +906,12 @@ hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream) {
   hipLaunchKernelGGL(wheel_offsets_kernel, dim3(4 * (uint32_t)num_cus), dim3(256), 0, stream, table);
   return hipGetLastError();
 }
+
+#ifdef DSE_TIMING
+extern "C" int dse_debug_timing(unsigned long long* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dse_timing), sizeof(dse_timing)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 namespace {
 
