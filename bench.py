@@ -140,9 +140,12 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    g0_ev, g1_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    g0_ev.record(stream)
     for i in range(a.steps):
         step(i)
+    g1_ev.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -176,6 +179,7 @@ def main():
                                    "mask resident in HBM" + (" [count-only diagnostic]" if a.no_mask else ""),
                        "N": N, "P": P, "cs": cs, "mask_bytes_per_gpu": 0 if a.no_mask else words * 8,
                        "parallelism": f"range-partition x{P} (RCCL broadcast + all-reduce)"},
+            "ms_per_step_gpu": g0_ev.elapsed_time(g1_ev) / a.steps,
             "pi_ref": pi_ref,
             "pi_full": pi_full,
             "verified": KNOWN_PI.get(N) == pi_full if N in KNOWN_PI else None,
