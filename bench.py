@@ -98,8 +98,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DSE_BENCH_REHEARSE=1: rehearsal of the N-rank code path on a 1-GPU box
+    # (gloo, every rank on cuda:0); its timings mean nothing.
+    rehearse = os.environ.get("DSE_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     P = world  # one spread-work chunk per GPU

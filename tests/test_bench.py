@@ -1,0 +1,57 @@
+"""bench.py's contract: one JSON line with the BASELINE metric, a roofline and
+cpu_baseline object, and pi verified; the N-rank path (broadcast, all-reduce,
+max-over-ranks timing) rehearsed with 2 ranks on one GPU over gloo
+(DSE_BENCH_REHEARSE=1; the driver's real N-GPU runs use RCCL)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _last_json(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    return json.loads(lines[0])
+
+
+def _check_line(d: dict, n_gpus: int):
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == n_gpus and d["verified"] is True and d["value"] > 0
+    rf = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in rf, k
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-6 * rf["frac"] + 1e-12
+
+
+@pytest.mark.gpu
+def test_bench_single_gpu_line():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--n", "1e10", "--steps", "2", "--warmup", "1",
+                        "--cpu-baseline", "on", "--cpu-sample-n", "1e8"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _last_json(r.stdout)
+    _check_line(d, 1)
+    assert d["cpu_baseline"]["cores"] == 1 and d["cpu_baseline"]["value"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_two_rank_rehearsal():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, DSE_BENCH_REHEARSE="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--n", "1e10", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _last_json(r.stdout)
+    _check_line(d, 2)
+    assert d["config"]["P"] == 2 and d["pi_full"] == 455052511
