@@ -404,6 +404,9 @@ __device__ __forceinline__ void unit_L(uint32_t* __restrict__ seg, const LargeOp
   const uint32_t n_min = (none || pmax >= KP) ? 0u : div_small(KP - pmax, pmax, fast_rcp((float)pmax));
   const uint32_t D = slow && live ? (uint32_t)(p2 - Vs) : 0u;
   if (!live) return;
+  // Primes above KP/2 mark branch-free: a predicated-off mark is an OR of 0 at
+  // an address inside the segment (mark_plane<true>); the per-plane branches it
+  // replaces cost more in exec-mask round trips than the extra LDS op (-1.2%).
 #pragma unroll
   for (uint32_t q = 0; q < 8; ++q) {
     const uint32_t t = o.a[q] + nKbm + ps.ne[q];
@@ -422,18 +425,17 @@ __device__ __forceinline__ void unit_L(uint32_t* __restrict__ seg, const LargeOp
     }
     const uint32_t pb32 = ps.pb[q];
     if (pmin > KP) {
-      if (kk < KP) mark_plane<false>(pb32, kk);
+      mark_plane<true>(pb32, kk);
     } else if (pmin > KP / 2) {
-      if (kk < KP) mark_plane<false>(pb32, kk);
-      kk += p;
-      if (kk < KP) mark_plane<false>(pb32, kk);
+      mark_plane<true>(pb32, kk);
+      mark_plane<true>(pb32, kk + p);
     } else {
 #pragma unroll 2
       for (uint32_t h = 0; h < n_min; ++h) {
         mark_plane<false>(pb32, kk);
         kk = opaque(kk + p);
       }
-      for (; kk < KP; kk += p) mark_plane<false>(pb32, kk);
+      for (; kk < KP; kk += p) mark_plane<false>(pb32, kk);  // a predicated fixed-count tail is slower
     }
   }
 }
