@@ -603,16 +603,25 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       // (by then this wave's marks of unit j have drained), and a large unit's
       // operands are loaded while the unit before it runs.
       const uint32_t n_int = min(n1, n2), n_all = n1 + n2;
+      // The claim is an asm ds_add_rtn: written as a C++ atomic, the AMDGPU
+      // atomic optimizer aggregates it over the wave and waits for its return
+      // on the spot (draining the previous unit's marks with it), which
+      // defeats the two-ahead issue (+1% kernel time). Read through claimed().
+      const uint32_t ctr_addr = lds_addr(&lds.ctr);
       auto claim = [&]() -> uint32_t {
         uint32_t j = 0;
-        if (lane == 0) j = atomicAdd(&lds.ctr, 1u);
+        if (lane == 0) asm volatile("ds_add_rtn_u32 %0, %1, %2" : "=v"(j) : "v"(ctr_addr), "v"(1u) : "memory");
         return j;  // per-lane value; lane 0 holds the claim
+      };
+      auto claimed = [&](uint32_t j) -> uint32_t {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(j)::"memory");
+        return __builtin_amdgcn_readlane(j, 0);
       };
       auto is_l = [&](uint32_t u) -> bool { return u < 2 * n_int ? (u & 1) != 0 : n2 > n1; };
       auto idx_of = [&](uint32_t u) -> uint32_t { return u < 2 * n_int ? u >> 1 : u - n_int; };
       LargeOps cur, nxt;
-      uint32_t u_cur = __builtin_amdgcn_readlane(claim(), 0);
-      uint32_t u_nxt = __builtin_amdgcn_readlane(claim(), 0);
+      uint32_t u_cur = claimed(claim());
+      uint32_t u_nxt = claimed(claim());
       if (u_cur < n_all && is_l(u_cur)) load_L(cur, P, M, A, i_mid1 + 64 * idx_of(u_cur) + lane, i_big);
       while (u_cur < n_all) {
         const uint32_t c2 = claim();  // unit after next, read at the end of this one
@@ -637,7 +646,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         }
         cur = nxt;
         u_cur = u_nxt;
-        u_nxt = __builtin_amdgcn_readlane(c2, 0);
+        u_nxt = claimed(c2);
       }
       // bucketed hits of the primes > kWheelMaxPrime: one entry per thread
       if (wa.bk_start && (phases & kPhaseLarge)) {
