@@ -39,7 +39,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=float, default=1e11, help="sieve limit N (default 1e11, the headline)")
+    ap.add_argument("--n", "--N", dest="n", type=float, default=1e11,
+                    help="sieve limit N (default 1e11, the headline); spell it --N under torch.distributed.run")
     ap.add_argument("--no-mask", action="store_true", help="count only (not the product path; diagnostics)")
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
     ap.add_argument("--cpu-sample-n", type=float, default=3e9)

@@ -35,6 +35,7 @@
 // See DESIGN.md section 4 for the rooflines.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -487,7 +488,11 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + table_a_offset(th->cap));
 
   const uint32_t tid = threadIdx.x, lane_id = tid & 63, wave = tid >> 6;
-  const uint32_t phases = wa.phases;
+#ifdef DSE_PHASE_KNOB
+  const uint32_t phases = wa.phases;  // ablation builds (tools/build_variant.sh knob -DDSE_PHASE_KNOB)
+#else
+  constexpr uint32_t phases = kPhaseAll;  // a runtime mask costs SGPRs (spill reloads in the unit loop): -0.5%
+#endif
 
   if (tid == 0) {
     // first index with p > 61, with p > TA, with p > TB (capped by the LDS stage)
@@ -930,6 +935,9 @@ namespace {
 WheelArgs make_wheel_args(uint64_t g_start, uint64_t nbits, uint64_t* plane_lut) {
   static const uint32_t phases = [] {
     const char* e = getenv("DSE_PHASES");  // profiling-only ablation knob
+#ifndef DSE_PHASE_KNOB
+    if (e) fprintf(stderr, "dse: DSE_PHASES ignored: this libdse.so was built without -DDSE_PHASE_KNOB\n");
+#endif
     return e ? (uint32_t)strtoul(e, nullptr, 0) & kPhaseAll : kPhaseAll;
   }();
   WheelArgs wa{};

@@ -49,7 +49,7 @@ def test_bench_two_rank_rehearsal():
     env = dict(os.environ, DSE_BENCH_REHEARSE="1")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-                        "--gpus", "2", "--n", "1e10", "--steps", "2", "--warmup", "1"],
+                        "--gpus", "2", "--N", "1e10", "--steps", "2", "--warmup", "1"],
                        capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     d = _last_json(r.stdout)

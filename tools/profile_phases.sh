@@ -4,6 +4,7 @@ set -u
 OUT=gpurun_out/prof_phases
 mkdir -p $OUT
 export TMPDIR=/tmp
+export DSE_LIB=${DSE_LIB:-variants/libdse_knob.so}  # knob build: tools/build_variant.sh knob -DDSE_PHASE_KNOB
 for v in ${VARIANTS:-127 121 122 124 120}; do
   for grp in "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVES" \
              "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE"; do

@@ -11,6 +11,8 @@ CLASSES = {1: (61, 1024), 2: (1024, 16384), 4: (16384, 1 << 40)}
 
 
 def run_one(g0, nb, phases):
+    from mail_sieve_e import _dse
+    _dse.LIB_PATH = os.environ.get("DSE_LIB", os.path.join(ROOT, "variants", "libdse_knob.so"))  # knob build
     from mail_sieve_e.sieve import Context
     from mail_sieve_e.work import odd_primes_upto
     c = Context(1)
