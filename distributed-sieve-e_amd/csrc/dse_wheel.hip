@@ -39,6 +39,8 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <mutex>
+#include <vector>
 
 #include "dse_internal.h"
 
@@ -987,27 +989,41 @@ uint64_t bucket_cap(uint64_t span, double a, double b) {
 
 constexpr uint64_t kBucketMaxEntries = 1ull << 31;  // 8 GB of entries per pass
 
-// Per-device scratch for the bucket pass (grow-only; freed with the process).
+// Scratch for the bucket pass, one grow-only buffer per (device, stream): work
+// on one stream is ordered, so a buffer is never used by two passes at once,
+// while two contexts sieving windows concurrently on one device (different
+// streams) get separate buffers. Freed with the process.
 struct Scratch {
-  void* ptr = nullptr;
-  uint64_t bytes = 0;
+  int dev;
+  hipStream_t stream;
+  void* ptr;
+  uint64_t bytes;
 };
-Scratch g_scratch[64];
+std::mutex g_scratch_mu;
+std::vector<Scratch> g_scratch;
 
-hipError_t bucket_scratch(uint64_t bytes, char** out) {
+hipError_t bucket_scratch(uint64_t bytes, hipStream_t stream, char** out) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
-  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-  Scratch& sc = g_scratch[dev];
-  if (sc.bytes < bytes) {
-    if (sc.ptr && (e = hipFree(sc.ptr)) != hipSuccess) return e;
-    sc.ptr = nullptr;
-    sc.bytes = 0;
-    if ((e = hipMalloc(&sc.ptr, bytes)) != hipSuccess) return e;
-    sc.bytes = bytes;
+  std::lock_guard<std::mutex> lock(g_scratch_mu);
+  Scratch* sc = nullptr;
+  for (Scratch& x : g_scratch)
+    if (x.dev == dev && x.stream == stream) sc = &x;
+  if (!sc) {
+    g_scratch.push_back(Scratch{dev, stream, nullptr, 0});
+    sc = &g_scratch.back();
   }
-  *out = static_cast<char*>(sc.ptr);
+  if (sc->bytes < bytes) {
+    // the stream's earlier passes may still read the old buffer
+    if (sc->ptr && ((e = hipStreamSynchronize(stream)) != hipSuccess || (e = hipFree(sc->ptr)) != hipSuccess))
+      return e;
+    sc->ptr = nullptr;
+    sc->bytes = 0;
+    if ((e = hipMalloc(&sc->ptr, bytes)) != hipSuccess) return e;
+    sc->bytes = bytes;
+  }
+  *out = static_cast<char*>(sc->ptr);
   return hipSuccess;
 }
 
@@ -1057,7 +1073,7 @@ hipError_t launch_sieve_range_wheel(const void* table, uint64_t g_start, uint64_
     const uint64_t o_cols = 256, o_tot = o_cols + 4ull * kBucketGrid * ns, o_start = o_tot + 4 * ns + 256,
                    o_ent = (o_start + 4 * (ns + 1) + 255) & ~255ull, bytes = o_ent + 4 * cap;
     char* sc = nullptr;
-    hipError_t e = bucket_scratch(bytes, &sc);
+    hipError_t e = bucket_scratch(bytes, stream, &sc);
     if (e != hipSuccess) return e;
     uint32_t* range = reinterpret_cast<uint32_t*>(sc);
     uint32_t* cols = reinterpret_cast<uint32_t*>(sc + o_cols);

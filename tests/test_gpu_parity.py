@@ -261,6 +261,32 @@ def test_window_1e18_full(ctx):
     assert total == parts == 241_272_176
 
 
+def test_window_two_contexts_concurrently(ctx):
+    """Two contexts (own streams) sieving bucketed windows on one device at
+    the same time: each stream has its own bucket scratch."""
+    import threading
+    from mail_sieve_e.sieve import Context
+    wins = [(10**18 + k * 10**9 + (1 if k else 0), 10**18 + (k + 1) * 10**9) for k in range(4)]
+    want = [ctx.sieve_window(lo, hi) for lo, hi in wins]
+    got, errs = [None] * 4, []
+
+    def work(i):
+        try:
+            with Context(num_gpus=1) as c:
+                for _ in range(3):
+                    got[i] = c.sieve_window(*wins[i])
+                    assert got[i] == want[i]
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert not errs, errs
+    assert got == want
+
+
 # ---- bucketed pass (primes > 2^21; SURVEY 8(a) a11) ----
 
 def test_bucket_threshold_window_vs_oracle(ctx, oracle):
