@@ -748,6 +748,21 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   }
 }
 
+// floor((2^64-1)/p) for 2 <= p < 2^32 without a 64-bit division: a double
+// quotient (relative error 2^-52, so off by < 2^11) corrected by the exact
+// remainder, itself below 2^43 in magnitude and so exact in a double.
+__device__ __forceinline__ uint64_t barrett_factor(uint32_t p) {
+  const double dp = (double)p;
+  uint64_t m = (uint64_t)(18446744073709551615.0 / dp);        // rounds 2^64-1 up to 2^64: may overshoot
+  if (m > ~0ull / 2) m = ~0ull / 2;                              // p >= 2: the true m < 2^63
+  int64_t r = (int64_t)(~0ull - m * (uint64_t)p);                // true remainder + (true m - m) * p
+  m += (int64_t)__builtin_floor((double)r / dp);
+  r = (int64_t)(~0ull - m * (uint64_t)p);
+  while (r < 0) { --m; r += p; }
+  while (r >= (int64_t)p) { ++m; r -= p; }
+  return m;
+}
+
 // m[i] = floor((2^64-1)/p) and the rotated wheel-offset row of every table
 // prime: a[8i + ((j - i) & 7)] = first k >= 0 with p | R30[j] + 30k (p >= 7).
 __global__ void wheel_offsets_kernel(void* __restrict__ table) {
@@ -758,8 +773,9 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
   uint32_t* A = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + table_a_offset(h->cap));
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t p = P[i];
-    const uint64_t m = ~0ull / p;
+    const uint64_t m = barrett_factor(p);
     M[i] = m;
+    if (p > kWheelMaxPrime) continue;  // bucketed primes: the walk needs m only, never the rows
     if (p < 7) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) A[8ull * i + j] = 0;
