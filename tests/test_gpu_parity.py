@@ -287,6 +287,18 @@ def test_window_two_contexts_concurrently(ctx):
     assert got == want
 
 
+def test_kb_float_quotient_boundary(ctx, oracle):
+    """The L units take Kb mod p from a float quotient while Kb = floor(V/30)
+    < 2^32 and from a 64-bit Barrett reduction above: a range straddling
+    V = 30 * 2^32 (segments on both sides) against the oracle."""
+    v = 30 * 2**32
+    g0 = (v - 3) // 2 - 3 * 1966080 + 12345
+    nb = 6 * 1966080 + 777
+    m, c = ctx.sieve_odd_range(g0, nb)
+    m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
+    assert c == c_ref and np.array_equal(m, m_ref)
+
+
 # ---- bucketed pass (primes > 2^21; SURVEY 8(a) a11) ----
 
 def test_bucket_threshold_window_vs_oracle(ctx, oracle):
