@@ -46,7 +46,11 @@ class GpuEngine:
         if ndev < 1:
             raise RuntimeError("no GPU visible: the HIP engine is required (no CPU fallback)")
         self.torch = torch
-        self.device = torch.device("cuda", (my_num - 1) % ndev)
+        # one process per GPU: the node-local index comes from DSE_DEVICE or
+        # LOCAL_RANK when a launcher sets them (needed when machines of several
+        # nodes join in arbitrary order), else from the machine number
+        local = os.environ.get("DSE_DEVICE", os.environ.get("LOCAL_RANK"))
+        self.device = torch.device("cuda", int(local) % ndev if local is not None else (my_num - 1) % ndev)
         torch.cuda.set_device(self.device)
         self.ctx = S.Context(device=self.device.index)
 
