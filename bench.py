@@ -3,8 +3,9 @@
 
 One step = the whole hot path for N over P = n_gpus chunks (spread-work,
 sieve.clj:15-34), with every rank's inputs already on its GPU:
-  rank 0 builds the base primes <= sqrt(N) on its GPU -> RCCL broadcast to the
-  other ranks (mirrors the reference's prime broadcast, sieve.clj:139) -> each
+  rank 0 builds the base primes <= sqrt(N) on its GPU -> RCCL broadcast of the
+  primes to the other ranks (mirrors the reference's prime broadcast,
+  sieve.clj:139), which derive Barrett factors and wheel offsets -> each
   rank sieves its chunk into an odd-only bitmask in HBM + count -> the last rank
   also sieves the dropped tail -> RCCL all-reduce of the counts.
 Single GPU: `python bench.py`; N GPUs: torch.distributed.run --nproc-per-node N.
@@ -120,6 +121,7 @@ def main():
     ctx = S.Context(device=local)
     limit = S.base_limit_for_range(0, P * cs + tail_n)
     tbytes = S.base_table_bytes(limit)
+    pbytes = S.base_table_prime_bytes(limit)  # the primes: all a broadcast needs to carry
     table = torch.empty(tbytes, dtype=torch.uint8, device=dev)
     counts = torch.zeros(2, dtype=torch.int64, device=dev)
     mask = None if a.no_mask else torch.empty(words, dtype=torch.int64, device=dev)
@@ -132,7 +134,9 @@ def main():
         if rank == 0:
             ctx.base_primes_dev_async(limit, table.data_ptr(), tbytes, sp)
         if world > 1:
-            dist.broadcast(table, src=0)
+            dist.broadcast(table[:pbytes], src=0)
+            if rank != 0:
+                ctx.base_table_finish_dev_async(limit, table.data_ptr(), tbytes, sp)
         if i is not None:
             ev[i][0].record(stream)
         ctx.sieve_range_dev_async(table.data_ptr(), g0, cs, mask.data_ptr() if mask is not None else 0,

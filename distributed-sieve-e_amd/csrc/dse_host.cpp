@@ -267,6 +267,18 @@ int32_t dse_base_primes_dev_async(dse_ctx* ctx, uint64_t limit, void* table_dev,
   return DSE_OK;
 }
 
+uint64_t dse_base_table_prime_bytes(uint64_t limit) { return 16ull + 4ull * prime_cap(limit); }
+
+int32_t dse_base_table_finish_dev_async(dse_ctx* ctx, uint64_t limit, void* table_dev, uint64_t table_bytes,
+                                        void* stream) {
+  if (!ctx || !table_dev) return fail(DSE_EINVAL, "null ctx or table");
+  if (table_bytes < dse_base_table_bytes(limit)) return fail(DSE_EINVAL, "table buffer too small");
+  if (limit > dse::kBigBaseLimitMax) return fail(DSE_ERANGE, "base-prime limit above the supported maximum");
+  HIP_TRY(hipSetDevice(ctx->devs[0].device));
+  HIP_TRY(dse::launch_wheel_offsets(table_dev, ctx->devs[0].num_cus, (hipStream_t)stream));
+  return DSE_OK;
+}
+
 int32_t dse_sieve_range_dev_async(dse_ctx* ctx, const void* table_dev, uint64_t g_start, uint64_t nbits,
                                   uint64_t* mask_dev, uint64_t* count_dev, void* stream) {
   if (!ctx || !table_dev || !count_dev) return fail(DSE_EINVAL, "null ctx, table or count");
@@ -368,17 +380,23 @@ int32_t dse_sieve_all(dse_ctx* ctx, int64_t n, int32_t P, uint64_t* per_chunk_co
   ctx->last_n = n;
   ctx->last_P = P;
 
-  // base primes once, on device 0; RCCL broadcast to the others
+  // base primes once, on device 0; RCCL broadcast of the primes to the
+  // others, which derive their Barrett factors and wheel offsets locally
   HIP_TRY(hipSetDevice(ctx->devs[0].device));
   if ((rc = build_table(ctx->devs[0], limit))) return rc;
-  const uint64_t tbytes = dse_base_table_bytes(limit);
+  const uint64_t pbytes = dse_base_table_prime_bytes(limit);
   if (nd > 1) {
     NCCL_TRY(ncclGroupStart());
     for (int i = 0; i < nd; ++i) {
       DevState& d = ctx->devs[i];
-      NCCL_TRY(ncclBroadcast(ctx->devs[0].table, d.table, tbytes, ncclUint8, 0, ctx->comms[i], d.stream));
+      NCCL_TRY(ncclBroadcast(ctx->devs[0].table, d.table, pbytes, ncclUint8, 0, ctx->comms[i], d.stream));
     }
     NCCL_TRY(ncclGroupEnd());
+    for (int i = 1; i < nd; ++i) {
+      DevState& d = ctx->devs[i];
+      HIP_TRY(hipSetDevice(d.device));
+      HIP_TRY(dse::launch_wheel_offsets(d.table, d.num_cus, d.stream));
+    }
   }
 
   // each device sieves its chunks; the last device also sieves the tail

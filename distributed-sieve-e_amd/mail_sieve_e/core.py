@@ -61,6 +61,14 @@ class GpuEngine:
         sp = self.torch.cuda.current_stream(self.device).cuda_stream
         self.ctx.base_primes_dev_async(limit, table.data_ptr(), table.numel(), sp)
 
+    def table_primes(self, limit: int, table):
+        """The part of the table a broadcast carries: header + primes."""
+        return table[: S.base_table_prime_bytes(limit)]
+
+    def finish_table(self, limit: int, table) -> None:
+        sp = self.torch.cuda.current_stream(self.device).cuda_stream
+        self.ctx.base_table_finish_dev_async(limit, table.data_ptr(), table.numel(), sp)
+
     def new_counts(self):
         return self.torch.zeros(2, dtype=self.torch.int64, device=self.device)
 
@@ -109,7 +117,9 @@ def _run_machine(store, my_num: int, num_comps: int, num_primes: int, engine, ou
         if rank == 0:
             engine.build_table(limit, table)                 # replaces per-prime sends (sieve.clj:139)
         if P > 1:
-            dist.broadcast(table, src=0)                     # replaces the lead's relay (core.clj:118-134)
+            dist.broadcast(engine.table_primes(limit, table), src=0)  # replaces the lead's relay (core.clj:118-134)
+            if rank != 0:
+                engine.finish_table(limit, table)
         counts = engine.new_counts()
         mask = engine.sieve(table, chunk.g_start, chunk.cs, counts, 0, want_mask=True)
         if rank == P - 1 and tail_n:

@@ -103,6 +103,11 @@ class Context:
         check(lib().dse_base_primes_dev_async(self.ptr, limit, table_ptr, table_bytes, stream_ptr or None),
               "dse_base_primes_dev_async")
 
+    def base_table_finish_dev_async(self, limit: int, table_ptr: int, table_bytes: int, stream_ptr: int = 0):
+        """Barrett factors + wheel offsets for a table whose primes arrived by broadcast."""
+        check(lib().dse_base_table_finish_dev_async(self.ptr, limit, table_ptr, table_bytes, stream_ptr or None),
+              "dse_base_table_finish_dev_async")
+
     def sieve_range_dev_async(self, table_ptr: int, g_start: int, nbits: int, mask_ptr: int,
                               count_ptr: int, stream_ptr: int = 0):
         check(lib().dse_sieve_range_dev_async(self.ptr, table_ptr, g_start, nbits, mask_ptr or None,
@@ -112,6 +117,11 @@ class Context:
 
 def base_table_bytes(limit: int) -> int:
     return int(lib().dse_base_table_bytes(limit))
+
+
+def base_table_prime_bytes(limit: int) -> int:
+    """Leading bytes of a base table that hold the primes: what ranks broadcast."""
+    return int(lib().dse_base_table_prime_bytes(limit))
 
 
 def base_limit_for_range(g_start: int, nbits: int) -> int:

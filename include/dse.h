@@ -141,6 +141,19 @@ uint64_t dse_base_limit_for_range(uint64_t g_start, uint64_t nbits);
 int32_t dse_base_primes_dev_async(dse_ctx *ctx, uint64_t limit, void *table_dev,
                                   uint64_t table_bytes, void *stream);
 
+/* Bytes at the start of a base-prime table that hold the primes themselves
+ * (header + p[]). Ranks broadcast only these (the reference's prime
+ * broadcast, sieve.clj:139 / core.clj:126) and complete the rest locally with
+ * dse_base_table_finish_dev_async. */
+uint64_t dse_base_table_prime_bytes(uint64_t limit);
+
+/* Complete a table of odd primes <= limit whose first
+ * dse_base_table_prime_bytes(limit) bytes are in place (e.g. received by
+ * broadcast): Barrett factors and mod-30 wheel offsets, on this context's
+ * device. Asynchronous on stream. */
+int32_t dse_base_table_finish_dev_async(dse_ctx *ctx, uint64_t limit, void *table_dev,
+                                        uint64_t table_bytes, void *stream);
+
 /* Sieve odd indices [g_start, g_start+nbits) with a base table on the device:
  * mask_dev (ceil(nbits/64) uint64 words, or NULL) receives the prime bits,
  * *count_dev (device uint64) is INCREMENTED by the prime count (zero it

@@ -38,6 +38,12 @@ class OracleEngine:
     def build_table(self, limit, table):
         table.copy_(self.torch.from_numpy(self._primes(limit)))
 
+    def table_primes(self, limit, table):
+        return table
+
+    def finish_table(self, limit, table):
+        pass
+
     def new_counts(self):
         return self.torch.zeros(2, dtype=self.torch.int64)
 

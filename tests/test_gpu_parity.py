@@ -287,6 +287,40 @@ def test_window_two_contexts_concurrently(ctx):
     assert got == want
 
 
+@pytest.mark.parametrize("limit", [316_227, 1_000_003, 5_000_011])
+def test_table_from_broadcast_primes(ctx, limit):
+    """Ranks receive only the primes (dse_base_table_prime_bytes) and finish
+    the table locally: same Barrett factors and offsets, same sieve."""
+    import torch
+    from mail_sieve_e import sieve as S
+    dev = torch.device("cuda", 0)
+    tbytes, pbytes = S.base_table_bytes(limit), S.base_table_prime_bytes(limit)
+    cap = (pbytes - 16) // 4
+    m_off = (16 + 4 * cap + 7) & ~7
+    a_off = (m_off + 8 * cap + 31) & ~31
+    full = torch.empty(tbytes, dtype=torch.uint8, device=dev)
+    ctx.base_primes_dev_async(limit, full.data_ptr(), tbytes, 0)
+    torch.cuda.synchronize()
+    part = torch.full((tbytes,), 0xA5, dtype=torch.uint8, device=dev)
+    part[:pbytes] = full[:pbytes]
+    ctx.base_table_finish_dev_async(limit, part.data_ptr(), tbytes, 0)
+    torch.cuda.synchronize()
+    n = int(full[:4].cpu().view(torch.int32)[0])
+    assert torch.equal(full[m_off:m_off + 8 * n], part[m_off:m_off + 8 * n])  # Barrett factors
+    P = full[16:16 + 4 * n].cpu().view(torch.int32).numpy()
+    n_rows = int(np.searchsorted(P, 1 << 21, side="right"))                 # rows exist for p <= 2^21
+    assert torch.equal(full[a_off:a_off + 32 * n_rows], part[a_off:a_off + 32 * n_rows])
+    g0, nb = (limit * limit) // 2 - 5_000_000, 4_000_000
+    outs = []
+    for t in (full, part):
+        mask = torch.zeros((nb + 63) // 64, dtype=torch.int64, device=dev)
+        cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+        ctx.sieve_range_dev_async(t.data_ptr(), g0, nb, mask.data_ptr(), cnt.data_ptr(), 0)
+        torch.cuda.synchronize()
+        outs.append((mask.cpu(), int(cnt.item())))
+    assert outs[0][1] == outs[1][1] > 0 and torch.equal(outs[0][0], outs[1][0])
+
+
 def test_kb_float_quotient_boundary(ctx, oracle):
     """The L units take Kb mod p from a float quotient while Kb = floor(V/30)
     < 2^32 and from a 64-bit Barrett reduction above: a range straddling
