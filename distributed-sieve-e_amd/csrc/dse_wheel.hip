@@ -21,6 +21,8 @@
 //
 // Per segment, one 1024-thread workgroup:
 //   1. init: every word = the OR of the patterns of 7..61 (register shifts);
+//      each wave inits the rows it expands, right after expanding the
+//      previous segment;
 //   2. mark (ds_or_b32), units handed out through an LDS counter:
 //      - A (61 < p <= LS/16): one prime per wave, lane L walks column L;
 //      - B (LS/16 < p <= LS): 8 primes x 8 planes per wave; lane (prime j,
@@ -559,6 +561,47 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   const uint64_t nseg = (wa.nbits + kWheelOutBits - 1) / kWheelOutBits;
   unsigned long long my_count = 0;
 
+  // ---- 1. init: small-prime patterns (7..61) of segment s. Wave w writes
+  // rows 32w..32w+31 of every column: exactly the rows its expand reads, so
+  // a wave may init segment s+1 right after expanding segment s.
+  auto init_segment = [&](uint64_t s) {
+    uint32_t lane = lane_id;
+    asm volatile("" : "+v"(lane));
+    const uint32_t C = lane, pl = lane >> 3, c = lane & 7;
+    const uint32_t rho = (uint32_t)(wa.rho_pack >> (5 * pl)) & 31u;
+    const uint32_t r0 = wave * (ROWS / NW);              // 32 rows per wave
+    const uint32_t k0 = c * LS + 32 * r0;                // first period of the lane's words
+    uint32_t res[kNQ];
+#pragma unroll
+    for (int j = 0; j < kNQ; ++j) {
+      const uint32_t q = kQ[j];
+      // (Vs + rho + 30 k0) mod q, Vs = V0 + s*W
+      const uint32_t wq = (uint32_t)(kWheelSpan % q);
+      const uint32_t sq = (uint32_t)(s % q);
+      const uint32_t x = ((uint32_t)wa.v0q[j] + sq * wq + rho + (30u * k0) % q) % q;
+      const uint32_t u = x ? q - x : 0u;
+      res[j] = (u * inv30_const(q)) % q;                 // first k >= k0 with q | value, minus k0
+    }
+    const bool on = phases & kPhaseSmall;
+#pragma unroll 2
+    for (uint32_t r = 0; r < ROWS / NW; r += 2) {
+      uint64_t w = 0;
+#pragma unroll
+      for (int j = 0; j < kNQ; ++j) {
+        const uint32_t q = kQ[j];
+        const uint32_t d = 64 % q;
+        w |= pat64(q) << res[j];
+        res[j] = res[j] >= d ? res[j] - d : res[j] + q - d;
+      }
+      if (!on) w = 0;
+      seg[(r0 + r) * 64 + C] = (uint32_t)w;
+      seg[(r0 + r + 1) * 64 + C] = (uint32_t)(w >> 32);
+    }
+    if (tid == 0) lds.ctr = 0;
+  };
+  if (blockIdx.x < nseg) init_segment(blockIdx.x);
+  __syncthreads();
+
   for (uint64_t s = blockIdx.x; s < nseg; s += gridDim.x) {
     const uint64_t Vs = wa.V0 + s * kWheelSpan;  // segment base value
     const uint64_t Vend = Vs + kWheelSpan;
@@ -568,41 +611,6 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     asm volatile("" : "+v"(lane));
 
     DSE_TSTAMP(0);
-    // ---- 1. init: small-prime patterns (7..61) -------------------------
-    {
-      const uint32_t C = lane, pl = lane >> 3, c = lane & 7;
-      const uint32_t rho = (uint32_t)(wa.rho_pack >> (5 * pl)) & 31u;
-      const uint32_t r0 = wave * (ROWS / NW);              // 32 rows per wave
-      const uint32_t k0 = c * LS + 32 * r0;                // first period of the lane's words
-      uint32_t res[kNQ];
-#pragma unroll
-      for (int j = 0; j < kNQ; ++j) {
-        const uint32_t q = kQ[j];
-        // (Vs + rho + 30 k0) mod q, Vs = V0 + s*W
-        const uint32_t wq = (uint32_t)(kWheelSpan % q);
-        const uint32_t sq = (uint32_t)(s % q);
-        const uint32_t x = ((uint32_t)wa.v0q[j] + sq * wq + rho + (30u * k0) % q) % q;
-        const uint32_t u = x ? q - x : 0u;
-        res[j] = (u * inv30_const(q)) % q;                 // first k >= k0 with q | value, minus k0
-      }
-      const bool on = phases & kPhaseSmall;
-#pragma unroll 2
-      for (uint32_t r = 0; r < ROWS / NW; r += 2) {
-        uint64_t w = 0;
-#pragma unroll
-        for (int j = 0; j < kNQ; ++j) {
-          const uint32_t q = kQ[j];
-          const uint32_t d = 64 % q;
-          w |= pat64(q) << res[j];
-          res[j] = res[j] >= d ? res[j] - d : res[j] + q - d;
-        }
-        if (!on) w = 0;
-        seg[(r0 + r) * 64 + C] = (uint32_t)w;
-        seg[(r0 + r + 1) * 64 + C] = (uint32_t)(w >> 32);
-      }
-      if (tid == 0) lds.ctr = 0;
-    }
-    __syncthreads();
     DSE_TSTAMP(1);
 
     // ---- 2. mark -------------------------------------------------------
@@ -747,6 +755,10 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         }
       }
     }
+    // init of this workgroup's next segment, on the rows this wave just
+    // expanded: no barrier in between, and waves drift into init while
+    // others still expand (-0.7%)
+    if (s + gridDim.x < nseg) init_segment(s + gridDim.x);
     __syncthreads();
     DSE_TSTAMP(4);
   }

@@ -18,7 +18,9 @@ mark_busy = t[:, :, 2] - t[:, :, 1]
 mark_wall = t[:, :, 3].max(axis=1) - t[:, :, 1].min(axis=1)
 exp = t[:, :, 4] - t[:, :, 3]
 seg = t[:, :, 4].max(axis=1)
-print("cycles per segment (median over WGs): total %d  init %d  mark wall %d  expand %d" % (
+# stamps: 0 = 1 = mark start (the segment's init ran at the end of the previous
+# iteration), 2 = mark done, 3 = after the barrier, 4 = expand + next init done
+print("cycles per segment (median over WGs): total %d  init %d  mark wall %d  expand+next init %d" % (
     np.median(seg), np.median(init_end.max(axis=1)), np.median(mark_wall), np.median(exp.max(axis=1))))
 print("mark busy per wave: min %d median %d max %d (median over WGs); imbalance max/mean = %.3f" % (
     np.median(mark_busy.min(axis=1)), np.median(np.median(mark_busy, axis=1)), np.median(mark_busy.max(axis=1)),
