@@ -83,6 +83,28 @@ constexpr uint32_t inv30_const(uint32_t q) {
   return 0;
 }
 
+// Init tables (DSE_INIT_TABLES): the 15 small primes in 7 groups G with
+// period M_G = prod(G). U_G[y] = 1 iff some q in G divides y. Plane i period k
+// holds the value Vs + rho_i + 30k, and q | Vs + rho_i + 30k <=> q | k + c_G
+// with c_G = (Vs + rho_i) * 30^{-1} mod M_G (gcd(30, M_G) = 1), so every plane
+// reads the same bit string at its own offset. Each table is padded with its
+// own continuation to M_G + 1024 + 64 bits, so a lane's 1024-period run never
+// wraps: word t is two funnel shifts of three consecutive dwords.
+// Off by default: bit-exact, but the kernel took 3.4x as long on MI355X (33.7
+// vs 9.97 ms at 1e11) whatever addresses the table reads used, so the cost is
+// not the reads themselves. Build with
+// -DDSE_INIT_TABLES=1 (tools/build_variant.sh) to A/B it.
+#ifndef DSE_INIT_TABLES
+#define DSE_INIT_TABLES 0
+#endif
+constexpr int kNG = 7;
+constexpr uint32_t kGQ[kNG][3] = {{7, 11, 13}, {17, 19, 1}, {23, 29, 1}, {31, 37, 1},
+                                  {41, 43, 1}, {47, 53, 1}, {59, 61, 1}};
+constexpr uint32_t gmod(int g) { return kGQ[g][0] * kGQ[g][1] * kGQ[g][2]; }
+constexpr uint32_t gdwords(int g) { return (gmod(g) + 1024 + 64 + 31) / 32; }
+constexpr uint32_t gbase(int g) { return g == 0 ? 0u : gbase(g - 1) + gdwords(g - 1); }
+constexpr uint32_t kInitDwords = gbase(kNG);  // 585 dwords
+
 struct WheelArgs {
   uint64_t V0;         // v_start - 1
   uint64_t nbits;      // odd candidates in the range
@@ -93,6 +115,7 @@ struct WheelArgs {
   uint32_t fix0;       // output word 0 bits of the primes 3..61 inside the range
   uint32_t phases;
   uint8_t v0q[kNQ];    // V0 mod q
+  uint16_t v0g[kNG];   // V0 mod M_G (init tables)
   const uint32_t* bk_entries;  // bucketed hits of the primes > kWheelMaxPrime (or null):
   const uint32_t* bk_start;    // segment s owns entries [bk_start[s], bk_start[s+1]), k | plane << 17
 };
@@ -464,6 +487,9 @@ struct WheelLds {
   uint64_t mid_m[kMidCap];         // Barrett factors of the staged mid primes
   uint32_t mid_p[kMidCap];         // p | (30^{-1} mod p) << 16
   uint32_t lut[256];               // period byte -> 15 odd slots
+#if DSE_INIT_TABLES
+  uint32_t itab[kInitDwords];      // small-prime group strings U_G (init)
+#endif
   uint32_t thr[4];
   uint32_t ctr;                    // dynamic unit counter of the current segment
   unsigned long long wave_cnt[NW];
@@ -537,6 +563,23 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     }
     s_lut[tid] = v;
   }
+#if DSE_INIT_TABLES
+#pragma unroll
+  for (int g = 0; g < kNG; ++g) {
+    if (tid >= gbase(g) && tid < gbase(g) + gdwords(g)) {
+      const uint32_t y0 = 32 * (tid - gbase(g));
+      uint32_t v = 0;
+#pragma unroll 1
+      for (uint32_t bit = 0; bit < 32; ++bit) {
+        const uint32_t y = y0 + bit;
+        bool hit = y % kGQ[g][0] == 0 || y % kGQ[g][1] == 0;
+        if (kGQ[g][2] > 1) hit = hit || y % kGQ[g][2] == 0;
+        v |= (uint32_t)hit << bit;
+      }
+      lds.itab[tid] = v;
+    }
+  }
+#endif
   __syncthreads();
   const uint32_t i_mid0 = s_thr[0], i_midB = s_thr[1], i_mid1 = s_thr[2];
   for (uint32_t i = tid; i < i_mid1 - i_mid0; i += NT) {
@@ -571,6 +614,35 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     const uint32_t rho = (uint32_t)(wa.rho_pack >> (5 * pl)) & 31u;
     const uint32_t r0 = wave * (ROWS / NW);              // 32 rows per wave
     const uint32_t k0 = c * LS + 32 * r0;                // first period of the lane's words
+    const bool on = phases & kPhaseSmall;
+#if DSE_INIT_TABLES
+    uint32_t ga[kNG], gsh[kNG], gd[kNG];
+#pragma unroll
+    for (int g = 0; g < kNG; ++g) {
+      const uint32_t Mg = gmod(g);
+      const uint32_t wg = (uint32_t)(kWheelSpan % Mg);
+      const uint32_t sg = (uint32_t)(s % Mg);
+      const uint32_t x = ((uint32_t)wa.v0g[g] + sg * wg + rho) % Mg;
+      const uint32_t off = (k0 + x * inv30_const(Mg)) % Mg;
+      ga[g] = gbase(g) + (off >> 5);
+      gsh[g] = off & 31;
+      gd[g] = lds.itab[ga[g]];
+    }
+#pragma unroll 2
+    for (uint32_t r = 0; r < ROWS / NW; r += 2) {
+      uint32_t lo = 0, hi = 0;
+#pragma unroll
+      for (int g = 0; g < kNG; ++g) {
+        const uint32_t d1 = lds.itab[ga[g] + r + 1], d2 = lds.itab[ga[g] + r + 2];
+        lo |= __builtin_amdgcn_alignbit(d1, gd[g], gsh[g]);
+        hi |= __builtin_amdgcn_alignbit(d2, d1, gsh[g]);
+        gd[g] = d2;
+      }
+      if (!on) lo = hi = 0;
+      seg[(r0 + r) * 64 + C] = lo;
+      seg[(r0 + r + 1) * 64 + C] = hi;
+    }
+#else
     uint32_t res[kNQ];
 #pragma unroll
     for (int j = 0; j < kNQ; ++j) {
@@ -582,7 +654,6 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       const uint32_t u = x ? q - x : 0u;
       res[j] = (u * inv30_const(q)) % q;                 // first k >= k0 with q | value, minus k0
     }
-    const bool on = phases & kPhaseSmall;
 #pragma unroll 2
     for (uint32_t r = 0; r < ROWS / NW; r += 2) {
       uint64_t w = 0;
@@ -597,6 +668,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       seg[(r0 + r) * 64 + C] = (uint32_t)w;
       seg[(r0 + r + 1) * 64 + C] = (uint32_t)(w >> 32);
     }
+#endif
     if (tid == 0) lds.ctr = 0;
   };
   if (blockIdx.x < nseg) init_segment(blockIdx.x);
@@ -1008,6 +1080,7 @@ WheelArgs make_wheel_args(uint64_t g_start, uint64_t nbits, uint64_t* plane_lut)
   for (uint32_t v : small)
     if (v >= v_start && (v - v_start) / 2 < nbits) wa.fix0 |= 1u << ((v - v_start) / 2);
   for (int j = 0; j < kNQ; ++j) wa.v0q[j] = (uint8_t)(wa.V0 % kQ[j]);
+  for (int g = 0; g < kNG; ++g) wa.v0g[g] = (uint16_t)(wa.V0 % gmod(g));
   wa.phases = phases;
   return wa;
 }
