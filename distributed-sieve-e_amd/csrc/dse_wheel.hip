@@ -563,7 +563,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     }
     s_lut[tid] = v;
   }
-#if DSE_INIT_TABLES && !defined(DSE_PROBE_NOBUILD)
+#if DSE_INIT_TABLES
 #pragma unroll
   for (int g = 0; g < kNG; ++g) {
     if (tid >= gbase(g) && tid < gbase(g) + gdwords(g)) {
@@ -621,11 +621,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     for (int g = 0; g < kNG; ++g) {
       const uint32_t Mg = gmod(g);
       const uint32_t wg = (uint32_t)(kWheelSpan % Mg);
-#ifdef DSE_PROBE_S32
-      const uint32_t sg = (uint32_t)s % Mg;
-#else
       const uint32_t sg = (uint32_t)(s % Mg);
-#endif
       const uint32_t x = ((uint32_t)wa.v0g[g] + sg * wg + rho) % Mg;
       const uint32_t off = (k0 + x * inv30_const(Mg)) % Mg;
       ga[g] = gbase(g) + (off >> 5);
@@ -834,9 +830,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     // init of this workgroup's next segment, on the rows this wave just
     // expanded: no barrier in between, and waves drift into init while
     // others still expand (-0.7%)
-#ifndef DSE_PROBE_NOINIT
     if (s + gridDim.x < nseg) init_segment(s + gridDim.x);
-#endif
     __syncthreads();
     DSE_TSTAMP(4);
   }
