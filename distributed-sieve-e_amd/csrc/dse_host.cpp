@@ -74,6 +74,7 @@ struct DevState {
   uint64_t* scratch_mask = nullptr;      // for dse_sieve_chunk
   uint64_t scratch_words = 0;
   std::vector<ChunkMask> resident;       // masks kept by dse_sieve_all
+  dse::Scratch scratch;                  // bucketed-pass scratch (high-offset ranges)
 };
 
 }  // namespace
@@ -83,6 +84,7 @@ struct dse_ctx {
   std::vector<ncclComm_t> comms;
   int64_t last_n = -1;
   int32_t last_P = 0;
+  dse::SieveOpts opts;  // test-only knobs (dse_debug_set_option)
 };
 
 namespace {
@@ -142,6 +144,44 @@ int32_t init_dev(DevState& d, int device) {
   HIP_TRY(hipGetDeviceProperties(&prop, device));
   d.num_cus = prop.multiProcessorCount;
   HIP_TRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  return DSE_OK;
+}
+
+// Base primes once, on device 0, then an RCCL broadcast of the primes (the
+// table's header + p[]) to the other devices, which derive their Barrett
+// factors and wheel offsets locally: the reference's prime broadcast
+// (sieve.clj:139, core.clj:94-95,126) done once. Every device's table buffer
+// must already hold dse_base_table_bytes(limit) bytes.
+int32_t share_table(dse_ctx* ctx, uint64_t limit) {
+  int32_t rc;
+  HIP_TRY(hipSetDevice(ctx->devs[0].device));
+  if ((rc = build_table(ctx->devs[0], limit))) return rc;
+  const int nd = (int)ctx->devs.size();
+  if (nd == 1) return DSE_OK;
+  const uint64_t pbytes = dse_base_table_prime_bytes(limit);
+  NCCL_TRY(ncclGroupStart());
+  for (int i = 0; i < nd; ++i) {
+    DevState& d = ctx->devs[i];
+    NCCL_TRY(ncclBroadcast(ctx->devs[0].table, d.table, pbytes, ncclUint8, 0, ctx->comms[i], d.stream));
+  }
+  NCCL_TRY(ncclGroupEnd());
+  for (int i = 1; i < nd; ++i) {
+    DevState& d = ctx->devs[i];
+    HIP_TRY(hipSetDevice(d.device));
+    HIP_TRY(dse::launch_wheel_offsets(d.table, d.num_cus, d.stream));
+  }
+  return DSE_OK;
+}
+
+// Sum `n` uint64 counts over the devices with an RCCL all-reduce (in place).
+int32_t allreduce_counts(dse_ctx* ctx, uint64_t n) {
+  if (ctx->devs.size() < 2) return DSE_OK;
+  NCCL_TRY(ncclGroupStart());
+  for (size_t i = 0; i < ctx->devs.size(); ++i) {
+    DevState& d = ctx->devs[i];
+    NCCL_TRY(ncclAllReduce(d.counts, d.counts, n, ncclUint64, ncclSum, ctx->comms[i], d.stream));
+  }
+  NCCL_TRY(ncclGroupEnd());
   return DSE_OK;
 }
 
@@ -216,6 +256,7 @@ void dse_destroy(dse_ctx* ctx) {
     if (d.table) (void)hipFree(d.table);
     if (d.counts) (void)hipFree(d.counts);
     if (d.scratch_mask) (void)hipFree(d.scratch_mask);
+    (void)dse::free_scratch(&d.scratch);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
   delete ctx;
@@ -287,7 +328,7 @@ int32_t dse_sieve_range_dev_async(dse_ctx* ctx, const void* table_dev, uint64_t 
   HIP_TRY(hipSetDevice(ctx->devs[0].device));
   HIP_TRY(dse::launch_sieve_range(table_dev, g_start, nbits, reinterpret_cast<uint32_t*>(mask_dev),
                                   reinterpret_cast<unsigned long long*>(count_dev), ctx->devs[0].num_cus,
-                                  (hipStream_t)stream));
+                                  (hipStream_t)stream, &ctx->devs[0].scratch, &ctx->opts));
   return DSE_OK;
 }
 
@@ -309,14 +350,13 @@ int32_t sieve_range_host(dse_ctx* ctx, DevState& d, uint64_t g0, uint64_t nbits,
   HIP_TRY(hipMemsetAsync(d.counts, 0, sizeof(unsigned long long), d.stream));
   HIP_TRY(dse::launch_sieve_range(d.table, g0, nbits,
                                   mask_or_null ? reinterpret_cast<uint32_t*>(d.scratch_mask) : nullptr,
-                                  d.counts, d.num_cus, d.stream));
+                                  d.counts, d.num_cus, d.stream, &d.scratch, &ctx->opts));
   unsigned long long c = 0;
   HIP_TRY(hipMemcpyAsync(&c, d.counts, sizeof(c), hipMemcpyDeviceToHost, d.stream));
   if (mask_or_null && words)
     HIP_TRY(hipMemcpyAsync(mask_or_null, d.scratch_mask, words * 8, hipMemcpyDeviceToHost, d.stream));
   HIP_TRY(hipStreamSynchronize(d.stream));
   if (count) *count = c;
-  (void)ctx;
   return DSE_OK;
 }
 }  // namespace
@@ -380,24 +420,7 @@ int32_t dse_sieve_all(dse_ctx* ctx, int64_t n, int32_t P, uint64_t* per_chunk_co
   ctx->last_n = n;
   ctx->last_P = P;
 
-  // base primes once, on device 0; RCCL broadcast of the primes to the
-  // others, which derive their Barrett factors and wheel offsets locally
-  HIP_TRY(hipSetDevice(ctx->devs[0].device));
-  if ((rc = build_table(ctx->devs[0], limit))) return rc;
-  const uint64_t pbytes = dse_base_table_prime_bytes(limit);
-  if (nd > 1) {
-    NCCL_TRY(ncclGroupStart());
-    for (int i = 0; i < nd; ++i) {
-      DevState& d = ctx->devs[i];
-      NCCL_TRY(ncclBroadcast(ctx->devs[0].table, d.table, pbytes, ncclUint8, 0, ctx->comms[i], d.stream));
-    }
-    NCCL_TRY(ncclGroupEnd());
-    for (int i = 1; i < nd; ++i) {
-      DevState& d = ctx->devs[i];
-      HIP_TRY(hipSetDevice(d.device));
-      HIP_TRY(dse::launch_wheel_offsets(d.table, d.num_cus, d.stream));
-    }
-  }
+  if ((rc = share_table(ctx, limit))) return rc;
 
   // each device sieves its chunks; the last device also sieves the tail
   for (int i = 0; i < nd; ++i) {
@@ -406,21 +429,15 @@ int32_t dse_sieve_all(dse_ctx* ctx, int64_t n, int32_t P, uint64_t* per_chunk_co
     for (auto& cm : d.resident) {
       const uint64_t g0 = (uint64_t)(cm.my_num - 1) * (uint64_t)cs;
       HIP_TRY(dse::launch_sieve_range(d.table, g0, (uint64_t)cs, reinterpret_cast<uint32_t*>(cm.dev_ptr),
-                                      d.counts + (cm.my_num - 1), d.num_cus, d.stream));
+                                      d.counts + (cm.my_num - 1), d.num_cus, d.stream, &d.scratch, &ctx->opts));
     }
     if (i == nd - 1 && tail_n)
-      HIP_TRY(dse::launch_sieve_range(d.table, tail_g, tail_n, nullptr, d.counts + P, d.num_cus, d.stream));
+      HIP_TRY(dse::launch_sieve_range(d.table, tail_g, tail_n, nullptr, d.counts + P, d.num_cus, d.stream,
+                                      &d.scratch, &ctx->opts));
   }
 
   // counts: RCCL all-reduce (each slot is non-zero on exactly one device)
-  if (nd > 1) {
-    NCCL_TRY(ncclGroupStart());
-    for (int i = 0; i < nd; ++i) {
-      DevState& d = ctx->devs[i];
-      NCCL_TRY(ncclAllReduce(d.counts, d.counts, nc, ncclUint64, ncclSum, ctx->comms[i], d.stream));
-    }
-    NCCL_TRY(ncclGroupEnd());
-  }
+  if ((rc = allreduce_counts(ctx, nc))) return rc;
   std::vector<unsigned long long> h(nc);
   HIP_TRY(hipSetDevice(ctx->devs[0].device));
   HIP_TRY(hipMemcpyAsync(h.data(), ctx->devs[0].counts, nc * sizeof(unsigned long long), hipMemcpyDeviceToHost,
@@ -470,23 +487,42 @@ int32_t dse_sieve_window(dse_ctx* ctx, uint64_t lo, uint64_t hi, uint64_t* count
     DevState& d = ctx->devs[i];
     HIP_TRY(hipSetDevice(d.device));
     if ((rc = ensure_counts(d, 1))) return rc;
-    if ((rc = build_table(d, limit))) return rc;
+    if ((rc = ensure_table(d, limit))) return rc;
     HIP_TRY(hipMemsetAsync(d.counts, 0, sizeof(unsigned long long), d.stream));
-    const uint64_t part = (nb + nd - 1) / nd;
-    const uint64_t s = std::min<uint64_t>(nb, part * i), e = std::min<uint64_t>(nb, part * (i + 1));
-    if (e > s) HIP_TRY(dse::launch_sieve_range(d.table, g0 + s, e - s, nullptr, d.counts, d.num_cus, d.stream));
   }
-  uint64_t total = 0;
+  // one table, built on device 0 and RCCL-broadcast (as dse_sieve_all)
+  if ((rc = share_table(ctx, limit))) return rc;
+  // contiguous slices of the window, one per device
+  const uint64_t part = (nb + nd - 1) / nd;
   for (int i = 0; i < nd; ++i) {
     DevState& d = ctx->devs[i];
     HIP_TRY(hipSetDevice(d.device));
-    unsigned long long c = 0;
-    HIP_TRY(hipMemcpyAsync(&c, d.counts, sizeof(c), hipMemcpyDeviceToHost, d.stream));
-    HIP_TRY(hipStreamSynchronize(d.stream));
-    total += c;
+    const uint64_t s = std::min<uint64_t>(nb, part * i), e = std::min<uint64_t>(nb, part * (i + 1));
+    if (e > s)
+      HIP_TRY(dse::launch_sieve_range(d.table, g0 + s, e - s, nullptr, d.counts, d.num_cus, d.stream, &d.scratch,
+                                      &ctx->opts));
   }
-  *count = total;
+  if ((rc = allreduce_counts(ctx, 1))) return rc;
+  unsigned long long c = 0;
+  HIP_TRY(hipSetDevice(ctx->devs[0].device));
+  HIP_TRY(hipMemcpyAsync(&c, ctx->devs[0].counts, sizeof(c), hipMemcpyDeviceToHost, ctx->devs[0].stream));
+  for (int i = 0; i < nd; ++i) {
+    HIP_TRY(hipSetDevice(ctx->devs[i].device));
+    HIP_TRY(hipStreamSynchronize(ctx->devs[i].stream));
+  }
+  *count = c;
   return DSE_OK;
+}
+
+int32_t dse_debug_set_option(dse_ctx* ctx, const char* name, int64_t value) {
+  if (!ctx || !name) return fail(DSE_EINVAL, "null ctx or option name");
+  const std::string n(name);
+  if (n == "bucket_pass_segments") {
+    if (value < 0 || value > 0xFFFFFFFFll) return fail(DSE_EINVAL, "bucket_pass_segments out of range");
+    ctx->opts.bucket_pass_segs = (uint32_t)value;
+    return DSE_OK;
+  }
+  return fail(DSE_EINVAL, "unknown option " + n);
 }
 
 }  // extern "C"

@@ -1,4 +1,4 @@
-// Internal interface between the gfx950 kernels (dse_kernels.hip) and the
+// Internal interface between the gfx950 kernels (dse_base.hip, dse_wheel.hip) and the
 // C-ABI host layer (dse_host.cpp). Not installed; include/dse.h is the ABI.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -32,18 +32,18 @@ __host__ __device__ inline uint64_t table_bytes_for_cap(uint32_t cap) {
 // The 8 residues mod 30 coprime to 30 (wheel planes, absolute numbering).
 constexpr uint32_t kR30[8] = {1, 7, 11, 13, 17, 19, 23, 29};
 
-// Mod-30 wheel segment geometry (dse_wheel.hip): 2^17 periods of 30 integers,
-// 8 planes (one per coprime residue) x 8 columns of 2^14 periods each.
-constexpr int kWheelLogKP = 17;
+// Mod-30 wheel segment geometry (dse_wheel.hip): a segment is 2^17 periods of
+// 30 integers, 8 planes (one per coprime residue) x 8 columns of 2^14 periods
+// (one 128 KiB LDS image). The two-image pipelined variant
+// (-DDSE_PIPELINE=1 -DDSE_WHEEL_LOG_KP=16) halves it.
+#ifndef DSE_WHEEL_LOG_KP
+#define DSE_WHEEL_LOG_KP 17
+#endif
+constexpr int kWheelLogKP = DSE_WHEEL_LOG_KP;
 constexpr uint64_t kWheelSpan = 30ull << kWheelLogKP;   // integers per segment
 constexpr uint64_t kWheelOutBits = kWheelSpan / 2;      // odd candidates per segment
 // Base primes above this go through the bucketed pass (dse_wheel.hip).
 constexpr uint64_t kWheelMaxPrime = 1ull << 21;
-
-// Segment geometry of the marking kernel (see DESIGN.md "Kernels").
-constexpr int kLogSeg = 20;               // 2^20 odd candidates per LDS segment (128 KiB)
-constexpr int kThreads = 1024;            // 16 waves per workgroup, one workgroup per CU
-constexpr int kSmallMax = 61;             // primes <= 61: register patterns at write-back
 
 // Largest limit the single-workgroup base-prime kernel handles (LDS bitmap).
 constexpr uint64_t kBaseLimitMax = 2ull * 150u * 1024u * 8u + 1ull;  // 150 KiB of odd bits
@@ -51,24 +51,37 @@ constexpr uint64_t kBaseLimitMax = 2ull * 150u * 1024u * 8u + 1ull;  // 150 KiB 
 // Big tables: odd primes < 2^31 (so p + SEG fits 32 bits in the kernel).
 constexpr uint64_t kBigBaseLimitMax = (1ull << 31) - 1;
 
+// Device scratch of one context (bucketed pass of high-offset ranges). Grows
+// on demand, freed by free_scratch (dse_destroy). `stream` is the stream of
+// the last pass that used it: a grow or a pass on another stream first waits
+// for that stream.
+struct Scratch {
+  void* ptr = nullptr;
+  uint64_t bytes = 0;
+  hipStream_t stream = nullptr;
+};
+hipError_t free_scratch(Scratch* s);
+
+// Test-only knobs, set through dse_debug_set_option (include/dse.h); the
+// defaults are the production configuration. No environment variable is read.
+struct SieveOpts {
+  uint32_t bucket_pass_segs = 0;  // > 0: cap the segments per bucket pass (multi-pass coverage)
+};
+
 hipError_t launch_base_primes(uint64_t limit, void* table, uint32_t cap, hipStream_t stream);
-// Any limit <= kBigBaseLimitMax: the one-workgroup kernel up to kBaseLimitMax,
-// above it a sieve of [3, limit] by the segment kernel + ordered compaction.
+// Any limit <= kBigBaseLimitMax: the multi-workgroup kernel up to kBaseLimitMax,
+// above it a sieve of [3, limit] by the wheel kernel + ordered compaction.
 hipError_t launch_base_primes_big(uint64_t limit, void* table, uint32_t cap, int num_cus, hipStream_t stream);
 
-// Sieve odd indices [g_start, g_start+nbits): out (may be null) gets the mask as
-// 32-bit words (2*ceil(nbits/64) of them, upper half of the last uint64 zeroed);
-// *count (device) is incremented.
+// Sieve odd indices [g_start, g_start+nbits) with the mod-30 wheel kernel: out
+// (may be null) gets the mask as 32-bit words (2*ceil(nbits/64) of them, upper
+// half of the last uint64 zeroed); *count (device) is incremented. Ranges whose
+// sqrt(max value) exceeds kWheelMaxPrime need `scratch` (bucketed pass);
+// `opts` may be null.
 hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
-                              unsigned long long* count, int num_cus, hipStream_t stream);
-
-// The two marking kernels behind launch_sieve_range: the odd-only kernel
-// (dse_kernels.hip) and the mod-30 wheel kernel (dse_wheel.hip).
-hipError_t launch_sieve_range_odd(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
-                                  unsigned long long* count, int num_cus, hipStream_t stream);
-hipError_t launch_sieve_range_wheel(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
-                                    unsigned long long* count, int num_cus, hipStream_t stream);
-// Fill the wheel offsets a[] of a table whose p[] and m[] are final.
+                              unsigned long long* count, int num_cus, hipStream_t stream, Scratch* scratch,
+                              const SieveOpts* opts);
+// Fill the Barrett factors m[] and wheel offsets a[] of a table whose p[] is final.
 hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream);
 
 }  // namespace dse

@@ -1,39 +1,40 @@
 // dse_wheel.hip -- mod-30 wheel segmented sieve for gfx950 (MI355X).
 //
-// Same contract as the odd-only kernel (dse_kernels.hip): bit j of the caller's
-// range stands for the odd value 3+2(g_start+j), the reference's element j of its
-// chunk vector (sieve.clj:9-13), and a set bit = prime. Only the LDS image
-// differs: multiples of 3 and 5 are never stored, so the marking loops (the
-// replacement of sieve.clj:36-71's index walk) touch 8/15 of the words the
-// odd-only image needs, and one 128 KiB segment covers 3,932,160 integers.
+// Bit j of the caller's range stands for the odd value 3+2(g_start+j), the
+// reference's element j of its chunk vector (sieve.clj:9-13); a set bit =
+// prime. The marking loops replace sieve.clj:36-71's index walk; multiples of
+// 3 and 5 are never stored in LDS, so they touch 8/15 of the words an odd-only
+// image needs.
 //
 // Geometry. V0 = v_start - 1 (even); segment s covers the integers
-// [Vs, Vs + 30*2^17) with Vs = V0 + s*30*2^17, which is exactly output bits
-// [s*1966080, (s+1)*1966080) -- a whole number of words, so no output word is
+// [Vs, Vs + W), W = 30*KP, Vs = V0 + s*W (KP = 2^17 periods), exactly output
+// bits [s*15*KP, (s+1)*15*KP) -- a whole number of words, so no output word is
 // shared by two segments. The 8 odd residues rho_0 < ... < rho_7 in [1,29]
 // with gcd(V0 + rho, 30) = 1 define the planes: plane i bit k <-> the value
 // Vs + rho_i + 30k, i.e. output bit 15k + (rho_i - 1)/2 of the segment.
 //
-// LDS image: plane i is split into 8 columns of LS = 2^14 periods; column
-// C = 8i + c holds periods [c*LS, (c+1)*LS) of plane i, 32 per word, and word
-// (row r, column C) sits at r*64 + C. The bank of a word is C mod 32 whatever
-// its row, so 32 lanes in 32 distinct columns never conflict.
+// LDS image (128 KiB): plane i is split into 8 columns of LS = KP/8 periods;
+// column C = 8i + c holds periods [c*LS, (c+1)*LS) of plane i, 32 per word,
+// and word (row r, column C) sits at r*64 + C. The bank of a word is C mod 32
+// whatever its row, so 32 lanes in 32 distinct columns never conflict.
 //
-// Per segment, one 1024-thread workgroup:
-//   1. init: every word = the OR of the patterns of 7..61 (register shifts);
-//      each wave inits the rows it expands, right after expanding the
-//      previous segment;
-//   2. mark (ds_or_b32), units handed out through an LDS counter:
-//      - A (61 < p <= LS/16): one prime per wave, lane L walks column L;
-//      - B (LS/16 < p <= LS): 8 primes x 8 planes per wave; lane (prime j,
-//        plane i) walks its plane's 8 columns diagonally (column (j+t) mod 8 at
-//        step t), so a half-wave touches 32 distinct columns at every step;
-//      - L (p > LS): one prime per lane, its 8 planes in a lane-rotated order,
-//        starts from the table's wheel offsets with one Barrett reduction;
-//   3. expand: lane reads one row of its column in all 8 planes, transposes the
-//      8x32 bits into 32 period bytes, maps each through a 256-entry LDS table
-//      to the 15 odd slots of its period, packs 480 output bits, fixes the
-//      small primes 3..61, masks the range end, popcounts, stores.
+// One workgroup of 1024 threads per CU, segments blockIdx.x + t*gridDim.x.
+// Per segment:
+//   1. mark (ds_or_b32), units taken from one LDS counter:
+//      A (61 < p <= TA): one prime per wave, lane L walks column L;
+//      B (TA < p <= TB): 8 primes x 8 planes per wave; lane (prime j, plane i)
+//        walks its plane's 8 columns diagonally (column (j+t) mod 8 at step t),
+//        so a half-wave touches 32 distinct columns at every step;
+//      L (p > TB): one prime per lane, its 8 planes in a lane-rotated order,
+//        starts from the table's wheel offsets with one reduction;
+//   2. expand: lane reads one row of its column in all 8 planes, transposes
+//      the 8x32 bits into 32 period bytes, maps each through a 256-entry LDS
+//      table to the 15 odd slots of its period, packs 480 output bits, fixes
+//      the small primes 3..61, masks the range end, popcounts, stores; then
+//      each wave inits (patterns of 7..61) the rows it expanded, for the next
+//      segment.
+// DSE_PIPELINE=1 (variant, slower: DESIGN.md section 4.1) uses two 64 KiB
+// images: expander waves expand/init one while the others mark the other.
 // See DESIGN.md section 4 for the rooflines.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -41,8 +42,6 @@
 #include <stdlib.h>
 
 #include <algorithm>
-#include <mutex>
-#include <vector>
 
 #include "dse_internal.h"
 
@@ -54,19 +53,36 @@ constexpr uint32_t kPhaseMidA = 1, kPhaseMidB = 2, kPhaseLarge = 4, kPhaseSmall 
 constexpr uint32_t kPhaseAll = 127;
 
 constexpr uint32_t KP = 1u << kWheelLogKP;  // periods per segment (per plane)
-constexpr uint32_t LOG_LS = 14;
+constexpr uint32_t LOG_LS = kWheelLogKP - 3;
 constexpr uint32_t LS = 1u << LOG_LS;       // periods per column
-constexpr uint32_t ROWS = LS / 32;          // 512 words per column
+constexpr uint32_t ROWS = LS / 32;          // words per column
+constexpr uint32_t IMG_WORDS = 64 * ROWS;   // one segment image
 constexpr uint32_t NT = 1024;
 constexpr uint32_t NW = NT / 64;
-constexpr uint32_t TA = LS / 16;            // A/B threshold
+#ifndef DSE_PIPELINE
+#define DSE_PIPELINE 0
+#endif
+#ifndef DSE_L_EXEC
+#define DSE_L_EXEC 0
+#endif
+#ifndef DSE_NE
+#define DSE_NE (DSE_PIPELINE ? 8 : 16)
+#endif
+constexpr uint32_t NIMG = DSE_PIPELINE ? 2 : 1;  // segment images in LDS
+constexpr uint32_t NE = DSE_NE;             // waves that expand and init
+static_assert(NE >= 1 && NE <= NW && (DSE_PIPELINE ? NE < NW : NE == NW) && ROWS % (8 * NE) == 0,
+              "expander rows");
+#ifndef DSE_TA
+#define DSE_TA (LS / 16)
+#endif
+constexpr uint32_t TA = DSE_TA;             // A/B threshold
 #ifndef DSE_TB
 #define DSE_TB 8192
 #endif
 constexpr uint32_t TB = DSE_TB;             // B/L threshold (<= LS)
 static_assert(TB <= LS && TB >= TA, "B/L threshold");
 constexpr uint32_t kMidCap = TB >= 16384 ? 1920 : TB >= 8192 ? 1040 : TB >= 4096 ? 580 : 320;  // odd primes in (61, TB]
-constexpr uint32_t kOutWordsPerSeg = (uint32_t)(kWheelOutBits / 32);  // 61440
+constexpr uint32_t kOutWordsPerSeg = (uint32_t)(kWheelOutBits / 32);  // 30720
 
 constexpr int kNQ = 15;
 constexpr uint32_t kQ[kNQ] = {7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61};
@@ -83,28 +99,6 @@ constexpr uint32_t inv30_const(uint32_t q) {
   return 0;
 }
 
-// Init tables (DSE_INIT_TABLES): the 15 small primes in 7 groups G with
-// period M_G = prod(G). U_G[y] = 1 iff some q in G divides y. Plane i period k
-// holds the value Vs + rho_i + 30k, and q | Vs + rho_i + 30k <=> q | k + c_G
-// with c_G = (Vs + rho_i) * 30^{-1} mod M_G (gcd(30, M_G) = 1), so every plane
-// reads the same bit string at its own offset. Each table is padded with its
-// own continuation to M_G + 1024 + 64 bits, so a lane's 1024-period run never
-// wraps: word t is two funnel shifts of three consecutive dwords.
-// Off by default: bit-exact, but the kernel took 3.4x as long on MI355X (33.7
-// vs 9.97 ms at 1e11) whatever addresses the table reads used, so the cost is
-// not the reads themselves. Build with
-// -DDSE_INIT_TABLES=1 (tools/build_variant.sh) to A/B it.
-#ifndef DSE_INIT_TABLES
-#define DSE_INIT_TABLES 0
-#endif
-constexpr int kNG = 7;
-constexpr uint32_t kGQ[kNG][3] = {{7, 11, 13}, {17, 19, 1}, {23, 29, 1}, {31, 37, 1},
-                                  {41, 43, 1}, {47, 53, 1}, {59, 61, 1}};
-constexpr uint32_t gmod(int g) { return kGQ[g][0] * kGQ[g][1] * kGQ[g][2]; }
-constexpr uint32_t gdwords(int g) { return (gmod(g) + 1024 + 64 + 31) / 32; }
-constexpr uint32_t gbase(int g) { return g == 0 ? 0u : gbase(g - 1) + gdwords(g - 1); }
-constexpr uint32_t kInitDwords = gbase(kNG);  // 585 dwords
-
 struct WheelArgs {
   uint64_t V0;         // v_start - 1
   uint64_t nbits;      // odd candidates in the range
@@ -115,9 +109,8 @@ struct WheelArgs {
   uint32_t fix0;       // output word 0 bits of the primes 3..61 inside the range
   uint32_t phases;
   uint8_t v0q[kNQ];    // V0 mod q
-  uint16_t v0g[kNG];   // V0 mod M_G (init tables)
   const uint32_t* bk_entries;  // bucketed hits of the primes > kWheelMaxPrime (or null):
-  const uint32_t* bk_start;    // segment s owns entries [bk_start[s], bk_start[s+1]), k | plane << 17
+  const uint32_t* bk_start;    // segment s owns entries [bk_start[s], bk_start[s+1]), k | plane << 16
 };
 
 __device__ __forceinline__ void lds_or(uint32_t* a, uint32_t v) {
@@ -130,10 +123,10 @@ __device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
 }
 
 // Mark period `off` of the column whose word 0 is at LDS byte address `cb`:
-// the segment is 256-byte aligned and a column's byte offset is < 256, so the
-// row offset (off >> 5) * 256 and the column combine with one v_and_or (the
-// compiler emits and + add). Issued as asm: callers drain lgkmcnt before a
-// barrier (lds_drain), since the compiler's waitcnt pass does not see it.
+// images are 64 KiB aligned and a column's byte offset is < 256, so the row
+// offset (off >> 5) * 256 (< 64 KiB) and the column combine with one v_and_or.
+// Issued as asm: callers drain lgkmcnt before a barrier (lds_drain), since the
+// compiler's waitcnt pass does not see it.
 __device__ __forceinline__ void mark_col(uint32_t cb, uint32_t off) {
   uint32_t a, b;
   asm volatile(
@@ -240,14 +233,12 @@ __device__ __forceinline__ uint32_t kmin_for(uint32_t D, uint32_t rho) {
 // 8 diagonal column steps of one lane's prime: per column n_u unconditional
 // marks and n_x value-predicated ones (wave-uniform counts, so the loop
 // control runs on the scalar unit); at the wrap from column 7 back to column 0
-// the offset restarts at the plane start O0. One instance for every count:
-// compile-time variants (~28 touched per segment) cost more in
-// instruction-cache misses than they save.
-__device__ __forceinline__ void diag_walk(uint32_t* __restrict__ seg, uint32_t off, uint32_t p, uint32_t cb,
+// the offset restarts at the plane start O0.
+__device__ __forceinline__ void diag_walk(uint32_t* __restrict__ img, uint32_t off, uint32_t p, uint32_t cb,
                                           uint32_t c, uint32_t O0, uint32_t n_u, uint32_t n_x) {
-  const uint32_t lds0 = lds_addr(seg);
+  const uint32_t lds0 = lds_addr(img);
   for (uint32_t t = 0; t < 8; ++t) {
-    uint32_t* colp = seg + cb + c;
+    uint32_t* colp = img + cb + c;
     const uint32_t cb_col = lds0 + 4 * (cb + c);
 #pragma unroll 2
     for (uint32_t h = 0; h < n_u; ++h) {
@@ -297,7 +288,7 @@ __device__ __forceinline__ void byte_transpose4(const uint32_t* P, uint32_t* T) 
 
 // A: one mid prime (61 < p <= TA) per wave; lane L walks column L =
 // (plane L>>3, column L&7).
-__device__ __forceinline__ void unit_A(uint32_t* __restrict__ seg, uint32_t pi, uint64_t m, uint64_t Vs,
+__device__ __forceinline__ void unit_A(uint32_t* __restrict__ img, uint32_t pi, uint64_t m, uint64_t Vs,
                                        uint64_t rho_pack, uint32_t lane) {
   const uint32_t p = pi & 0xFFFFu, inv30 = pi >> 16;  // wave-uniform
   const uint64_t p2 = (uint64_t)p * p;
@@ -306,7 +297,7 @@ __device__ __forceinline__ void unit_A(uint32_t* __restrict__ seg, uint32_t pi, 
   const uint32_t pl = lane >> 3, c = lane & 7;
   const uint32_t rho = (uint32_t)(rho_pack >> (5 * pl)) & 31u;
   const uint32_t kp = plane_first(Xs, rho, p, inv30, invp);
-  const uint32_t cb_col = lds_addr(seg) + 4 * lane;
+  const uint32_t cb_col = lds_addr(img) + 4 * lane;
   if (p2 <= Vs) {
     const uint32_t cm = mod_small(c * LS, p, invp);
     uint32_t off = kp >= cm ? kp - cm : kp + p - cm;
@@ -327,7 +318,7 @@ __device__ __forceinline__ void unit_A(uint32_t* __restrict__ seg, uint32_t pi, 
 // B: 8 mid primes (TA < p <= LS) x 8 planes; half-wave g takes planes
 // 4g..4g+3, lane (prime jp, plane pl) walks columns jp, jp+1, ... (mod 8):
 // at every step a half-wave is in 32 distinct columns.
-__device__ __forceinline__ void unit_B(uint32_t* __restrict__ seg, const uint32_t* __restrict__ s_mid_p,
+__device__ __forceinline__ void unit_B(uint32_t* __restrict__ img, const uint32_t* __restrict__ s_mid_p,
                                        const uint64_t* __restrict__ s_mid_m, uint32_t j0, uint32_t nj, uint64_t Vs,
                                        uint64_t Vend, uint64_t rho_pack, uint32_t lane) {
   const uint32_t pfirst = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
@@ -363,7 +354,7 @@ __device__ __forceinline__ void unit_B(uint32_t* __restrict__ seg, const uint32_
   // lanes past the batch end mark nothing (their unconditional marks would
   // land in another prime's columns)
   if (!valid) return;
-  diag_walk(seg, off, p, cb, jp, O0, n_u, n_x);
+  diag_walk(img, off, p, cb, jp, O0, n_u, n_x);
 }
 
 // Operands of one large unit, loaded ahead of use. The table row of prime i
@@ -386,13 +377,14 @@ __device__ __forceinline__ void load_L(LargeOps& o, const uint32_t* __restrict__
   o.a[4] = hi.x; o.a[5] = hi.y; o.a[6] = hi.z; o.a[7] = hi.w;
 }
 
-// Mark plane-relative period kk of plane byte base pb32 = lds0 + 32 * plane:
-// word (row (kk >> 5) & 511, column 8 * plane + ((kk >> 14) & 7)). The masks
-// keep any kk inside the segment, so a predicated-off mark (PRED and kk >= KP)
-// is an OR of 0 at a valid address. asm for the same reason as mark_col.
+// Mark plane-relative period kk of plane byte base pb32 = image + 32 * plane:
+// word (row (kk >> 5) & (ROWS-1), column 8 * plane + ((kk >> LOG_LS) & 7)).
+// The masks keep any kk inside the image, so a predicated-off mark (PRED and
+// kk >= KP) is an OR of 0 at a valid address. asm for the same reason as
+// mark_col.
 template <bool PRED>
 __device__ __forceinline__ void mark_plane(uint32_t pb32, uint32_t kk) {
-  const uint32_t col = __builtin_amdgcn_ubfe(kk, 14, 3);
+  const uint32_t col = __builtin_amdgcn_ubfe(kk, LOG_LS, 3);
   uint32_t bit = 1u << (kk & 31);
   if (PRED) bit = kk < KP ? bit : 0u;
   uint32_t a, t;
@@ -402,7 +394,7 @@ __device__ __forceinline__ void mark_plane(uint32_t pb32, uint32_t kk) {
       "v_and_or_b32 %0, %0, %5, %1\n\t"
       "ds_or_b32 %0, %6"
       : "=&v"(a), "=&v"(t)
-      : "v"(col), "v"(pb32), "v"(kk), "s"(0x1FF00u), "v"(bit)
+      : "v"(col), "v"(pb32), "v"(kk), "s"((ROWS - 1) << 8), "v"(bit)
       : "memory");
 }
 
@@ -418,8 +410,8 @@ struct PlaneSteps {
   uint32_t ne[8];
 };
 
-__device__ __forceinline__ void unit_L(uint32_t* __restrict__ seg, const LargeOps& o, uint64_t Vs, uint64_t Vend,
-                                       uint64_t Kb, const PlaneSteps& ps, uint32_t pl_rot, uint64_t rho_pack) {
+__device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t Vend, uint64_t Kb,
+                                       const PlaneSteps& ps, uint32_t pl_rot, uint64_t rho_pack) {
   const uint32_t p = o.p;
   const uint64_t p2 = (uint64_t)p * p;
   const bool live = p2 < Vend;
@@ -429,7 +421,7 @@ __device__ __forceinline__ void unit_L(uint32_t* __restrict__ seg, const LargeOp
   // quotient is within one of the true one (|error| < 0.11: Kb's rounding to
   // float <= 128/p, the rcp and the product 2^-23 of q < 2^19 for p > TB),
   // corrected by two unsigned min steps; the 64-bit Barrett reduction covers
-  // the rest. -1.3% kernel time at 1e11.
+  // the rest.
   uint32_t kbm;
   if (Kb < (1ull << 32)) {
     const uint32_t q = (uint32_t)((float)(uint32_t)Kb * invp);
@@ -447,8 +439,7 @@ __device__ __forceinline__ void unit_L(uint32_t* __restrict__ seg, const LargeOp
   const uint32_t D = slow && live ? (uint32_t)(p2 - Vs) : 0u;
   if (!live) return;
   // Primes above KP/2 mark branch-free: a predicated-off mark is an OR of 0 at
-  // an address inside the segment (mark_plane<true>); the per-plane branches it
-  // replaces cost more in exec-mask round trips than the extra LDS op (-1.2%).
+  // an address inside the image (mark_plane<true>).
 #pragma unroll
   for (uint32_t q = 0; q < 8; ++q) {
     const uint32_t t = o.a[q] + nKbm + ps.ne[q];
@@ -466,12 +457,21 @@ __device__ __forceinline__ void unit_L(uint32_t* __restrict__ seg, const LargeOp
       }
     }
     const uint32_t pb32 = ps.pb[q];
+#if DSE_L_EXEC  // variant: exec-masked instead of predicated (OR 0) marks
+    if (pmin > KP) {
+      if (kk < KP) mark_plane<false>(pb32, kk);
+    } else if (pmin > KP / 2) {
+      if (kk < KP) mark_plane<false>(pb32, kk);
+      if (kk + p < KP) mark_plane<false>(pb32, kk + p);
+    } else {
+#else
     if (pmin > KP) {
       mark_plane<true>(pb32, kk);
     } else if (pmin > KP / 2) {
       mark_plane<true>(pb32, kk);
       mark_plane<true>(pb32, kk + p);
     } else {
+#endif
 #pragma unroll 2
       for (uint32_t h = 0; h < n_min; ++h) {
         mark_plane<false>(pb32, kk);
@@ -483,45 +483,25 @@ __device__ __forceinline__ void unit_L(uint32_t* __restrict__ seg, const LargeOp
 }
 
 struct WheelLds {
-  uint32_t seg[KP * 8 / 32];       // the segment image (128 KiB)
+  uint32_t img[NIMG][IMG_WORDS];   // the segment image(s), at LDS address 0
   uint64_t mid_m[kMidCap];         // Barrett factors of the staged mid primes
   uint32_t mid_p[kMidCap];         // p | (30^{-1} mod p) << 16
   uint32_t lut[256];               // period byte -> 15 odd slots
-#if DSE_INIT_TABLES
-  uint32_t itab[kInitDwords];      // small-prime group strings U_G (init)
-#endif
   uint32_t thr[4];
-  uint32_t ctr;                    // dynamic unit counter of the current segment
+  uint32_t ctr[2];                 // unit counters (pipelined: one per image)
   unsigned long long wave_cnt[NW];
 };
-
-#ifdef DSE_TIMING
-// Debug build only: per-wave cycle stamps at the phase boundaries of segment
-// index 5 of each workgroup -> dse_timing[block][wave][5] (tools/wave_timing.py).
-__device__ unsigned long long dse_timing[256 * 16 * 5];
-#define DSE_TSTAMP(i)                                                                          \
-  do {                                                                                         \
-    if (s == blockIdx.x + 5ull * gridDim.x && lane_id == 0 && blockIdx.x < 256)                 \
-      dse_timing[(blockIdx.x * 16 + wave) * 5 + (i)] = __builtin_readcyclecounter();            \
-  } while (0)
-#else
-#define DSE_TSTAMP(i) \
-  do {                \
-  } while (0)
-#endif
 
 __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restrict__ table, WheelArgs wa,
                                                             uint32_t* __restrict__ out,
                                                             unsigned long long* __restrict__ count_out) {
-  // One static LDS object, so the segment image sits at LDS address 0
-  // (mark_col combines row and column offsets with a bitwise or).
+  // One static LDS object, so the images sit at LDS addresses 0 and 64 KiB
+  // (mark_col / mark_plane combine row and column offsets with a bitwise or).
   __shared__ WheelLds lds;
-  uint32_t* const seg = lds.seg;
   uint64_t* const s_mid_m = lds.mid_m;
   uint32_t* const s_mid_p = lds.mid_p;
   uint32_t* const s_lut = lds.lut;
   uint32_t* const s_thr = lds.thr;
-  unsigned long long* const s_wave_cnt = lds.wave_cnt;
 
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
   const uint32_t np = th->count;
@@ -532,10 +512,11 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + table_a_offset(th->cap));
 
   const uint32_t tid = threadIdx.x, lane_id = tid & 63, wave = tid >> 6;
+  const bool expander = wave < NE;
 #ifdef DSE_PHASE_KNOB
   const uint32_t phases = wa.phases;  // ablation builds (tools/build_variant.sh knob -DDSE_PHASE_KNOB)
 #else
-  constexpr uint32_t phases = kPhaseAll;  // a runtime mask costs SGPRs (spill reloads in the unit loop): -0.5%
+  constexpr uint32_t phases = kPhaseAll;  // a runtime mask costs SGPRs (spill reloads in the unit loop)
 #endif
 
   if (tid == 0) {
@@ -553,6 +534,8 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     hi = np;  // primes above kWheelMaxPrime are bucketed (or absent)
     while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= kWheelMaxPrime) lo = mid + 1; else hi = mid; }
     s_thr[3] = lo;
+    lds.ctr[0] = 0;
+    lds.ctr[1] = 0;
   }
   if (tid < 256) {
     uint32_t v = 0;
@@ -563,23 +546,6 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     }
     s_lut[tid] = v;
   }
-#if DSE_INIT_TABLES
-#pragma unroll
-  for (int g = 0; g < kNG; ++g) {
-    if (tid >= gbase(g) && tid < gbase(g) + gdwords(g)) {
-      const uint32_t y0 = 32 * (tid - gbase(g));
-      uint32_t v = 0;
-#pragma unroll 1
-      for (uint32_t bit = 0; bit < 32; ++bit) {
-        const uint32_t y = y0 + bit;
-        bool hit = y % kGQ[g][0] == 0 || y % kGQ[g][1] == 0;
-        if (kGQ[g][2] > 1) hit = hit || y % kGQ[g][2] == 0;
-        v |= (uint32_t)hit << bit;
-      }
-      lds.itab[tid] = v;
-    }
-  }
-#endif
   __syncthreads();
   const uint32_t i_mid0 = s_thr[0], i_midB = s_thr[1], i_mid1 = s_thr[2];
   for (uint32_t i = tid; i < i_mid1 - i_mid0; i += NT) {
@@ -589,10 +555,9 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   }
   // Work units: list 1 = nA single mid primes, then nB diagonal units (8
   // primes each); list 2 = nL large units (64 primes each); handed out through
-  // one dynamic queue (mark phase below). Issue arbitration favours older
-  // waves, so any static split finishes the youngest waves last (1.17x the
-  // mean on equal shares, measured with DSE_TIMING); the queue makes them take
-  // fewer units instead.
+  // one dynamic queue per image. Issue arbitration favours older waves, so
+  // any static split finishes the youngest waves last; the queue makes them
+  // take fewer units instead, and lets the expanders join when done.
   const uint32_t nA = i_midB - i_mid0;
   const uint32_t n_mid = i_mid1 - i_mid0;
   const uint32_t nB = (i_mid1 - i_midB + 7) / 8;
@@ -602,47 +567,21 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
 
   const uint64_t out_words = 2ull * ((wa.nbits + 63) / 64);  // 32-bit words of the caller's mask
   const uint64_t nseg = (wa.nbits + kWheelOutBits - 1) / kWheelOutBits;
+  const uint64_t grid = gridDim.x;
+  const uint32_t T = blockIdx.x < nseg ? (uint32_t)((nseg - 1 - blockIdx.x) / grid + 1) : 0u;  // rounds
   unsigned long long my_count = 0;
 
-  // ---- 1. init: small-prime patterns (7..61) of segment s. Wave w writes
-  // rows 32w..32w+31 of every column: exactly the rows its expand reads, so
-  // a wave may init segment s+1 right after expanding segment s.
-  auto init_segment = [&](uint64_t s) {
+  // ---- init: small-prime patterns (7..61) of segment s into an image.
+  // Expander wave w writes rows w*ROWS/NE .. +ROWS/NE of every column: the
+  // rows it expands, so it may init an image right after expanding it.
+  auto init_segment = [&](uint32_t* __restrict__ img, uint64_t s) {
     uint32_t lane = lane_id;
     asm volatile("" : "+v"(lane));
     const uint32_t C = lane, pl = lane >> 3, c = lane & 7;
     const uint32_t rho = (uint32_t)(wa.rho_pack >> (5 * pl)) & 31u;
-    const uint32_t r0 = wave * (ROWS / NW);              // 32 rows per wave
+    const uint32_t r0 = wave * (ROWS / NE);
     const uint32_t k0 = c * LS + 32 * r0;                // first period of the lane's words
     const bool on = phases & kPhaseSmall;
-#if DSE_INIT_TABLES
-    uint32_t ga[kNG], gsh[kNG], gd[kNG];
-#pragma unroll
-    for (int g = 0; g < kNG; ++g) {
-      const uint32_t Mg = gmod(g);
-      const uint32_t wg = (uint32_t)(kWheelSpan % Mg);
-      const uint32_t sg = (uint32_t)(s % Mg);
-      const uint32_t x = ((uint32_t)wa.v0g[g] + sg * wg + rho) % Mg;
-      const uint32_t off = (k0 + x * inv30_const(Mg)) % Mg;
-      ga[g] = gbase(g) + (off >> 5);
-      gsh[g] = off & 31;
-      gd[g] = lds.itab[ga[g]];
-    }
-#pragma unroll 2
-    for (uint32_t r = 0; r < ROWS / NW; r += 2) {
-      uint32_t lo = 0, hi = 0;
-#pragma unroll
-      for (int g = 0; g < kNG; ++g) {
-        const uint32_t d1 = lds.itab[ga[g] + r + 1], d2 = lds.itab[ga[g] + r + 2];
-        lo |= __builtin_amdgcn_alignbit(d1, gd[g], gsh[g]);
-        hi |= __builtin_amdgcn_alignbit(d2, d1, gsh[g]);
-        gd[g] = d2;
-      }
-      if (!on) lo = hi = 0;
-      seg[(r0 + r) * 64 + C] = lo;
-      seg[(r0 + r + 1) * 64 + C] = hi;
-    }
-#else
     uint32_t res[kNQ];
 #pragma unroll
     for (int j = 0; j < kNQ; ++j) {
@@ -655,7 +594,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       res[j] = (u * inv30_const(q)) % q;                 // first k >= k0 with q | value, minus k0
     }
 #pragma unroll 2
-    for (uint32_t r = 0; r < ROWS / NW; r += 2) {
+    for (uint32_t r = 0; r < ROWS / NE; r += 2) {
       uint64_t w = 0;
 #pragma unroll
       for (int j = 0; j < kNQ; ++j) {
@@ -665,183 +604,206 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         res[j] = res[j] >= d ? res[j] - d : res[j] + q - d;
       }
       if (!on) w = 0;
-      seg[(r0 + r) * 64 + C] = (uint32_t)w;
-      seg[(r0 + r + 1) * 64 + C] = (uint32_t)(w >> 32);
+      img[(r0 + r) * 64 + C] = (uint32_t)w;
+      img[(r0 + r + 1) * 64 + C] = (uint32_t)(w >> 32);
     }
-#endif
-    if (tid == 0) lds.ctr = 0;
   };
-  if (blockIdx.x < nseg) init_segment(blockIdx.x);
-  __syncthreads();
 
-  for (uint64_t s = blockIdx.x; s < nseg; s += gridDim.x) {
+  // ---- expand segment s (image img) to odd-only bits, count, store: lane
+  // (column c, row) of expander wave w reads that row of column c in all 8
+  // planes, rows 8 * (ROWS/(8 NE) * w + t) + (lane & 7).
+  auto expand_segment = [&](const uint32_t* __restrict__ img, uint64_t s) {
+    uint32_t lane = lane_id;
+    asm volatile("" : "+v"(lane));
+    const uint32_t c = lane >> 3, a8 = lane & 7;
+    const uint64_t seg_word0 = s * (uint64_t)kOutWordsPerSeg;
+#pragma unroll 1
+    for (uint32_t t = 0; t < ROWS / (NE * 8); ++t) {
+      const uint32_t row = 8 * ((ROWS / (NE * 8)) * wave + t) + a8;
+      const uint32_t* rp = img + row * 64 + c;
+      uint32_t Q[8];
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j) Q[j] = ~rp[8 * ((j + a8) & 7)];  // plane (j + a8) & 7, 1 = prime
+      // un-rotate by a8 (plane i = Q[(i - a8) & 7]): three conditional rotations
+      uint32_t R1[8], R2[8], Pw[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) R1[i] = (a8 & 1) ? Q[(i + 7) & 7] : Q[i];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) R2[i] = (a8 & 2) ? R1[(i + 6) & 7] : R1[i];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) Pw[i] = (a8 & 4) ? R2[(i + 4) & 7] : R2[i];
+      uint32_t TL[4], TH[4];
+      byte_transpose4(Pw, TL);
+      byte_transpose4(Pw + 4, TH);
+      uint32_t o[15];
+#pragma unroll
+      for (int w = 0; w < 15; ++w) o[w] = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t x = transpose8((uint64_t)TL[q] | ((uint64_t)TH[q] << 32));
+#pragma unroll
+        for (int bb = 0; bb < 8; ++bb) {
+          const uint32_t e = s_lut[(uint32_t)(x >> (8 * bb)) & 0xFFu];
+          const int pos = 15 * (8 * q + bb);
+          o[pos >> 5] |= e << (pos & 31);
+          if ((pos & 31) > 17) o[(pos >> 5) + 1] |= e >> (32 - (pos & 31));
+        }
+      }
+      const uint64_t w0 = seg_word0 + 15ull * (c * ROWS + row);  // caller's 32-bit word index
+      if (s == 0 && c == 0 && row == 0) o[0] |= wa.fix0;
+      const uint64_t bit0 = 32ull * w0;
+      if (bit0 + 480 > wa.nbits) {  // range end (last segment only)
+        const uint32_t rem = bit0 >= wa.nbits ? 0u : (uint32_t)(wa.nbits - bit0);  // < 480 valid bits
+#pragma unroll
+        for (int w = 0; w < 15; ++w) {
+          const uint32_t b = 32u * w;
+          o[w] = b >= rem ? 0u : (rem - b >= 32 ? o[w] : o[w] & ((1u << (rem - b)) - 1u));
+        }
+      }
+      uint32_t cnt = 0;
+#pragma unroll
+      for (int w = 0; w < 15; ++w) cnt += __popc(o[w]);
+      my_count += cnt;
+      if (out && (phases & kPhaseStore)) {
+        if (w0 + 15 <= out_words) {
+#pragma unroll
+          for (int w = 0; w < 15; ++w) out[w0 + w] = o[w];
+        } else {
+#pragma unroll
+          for (int w = 0; w < 15; ++w)
+            if (w0 + w < out_words) out[w0 + w] = o[w];
+        }
+      }
+    }
+  };
+
+  // ---- mark segment s into image img, units from counter ctr_i ------------
+  auto mark_segment = [&](uint32_t* __restrict__ img, uint64_t s, uint32_t ctr_i) {
     const uint64_t Vs = wa.V0 + s * kWheelSpan;  // segment base value
     const uint64_t Vend = Vs + kWheelSpan;
     // Lane-derived values are segment-invariant; left visible, the compiler
-    // hoists dozens of them out of this loop and spills them. Recompute instead.
+    // hoists dozens of them out of the round loop and spills them. Recompute.
     uint32_t lane = lane_id;
     asm volatile("" : "+v"(lane));
-
-    DSE_TSTAMP(0);
-    DSE_TSTAMP(1);
-
-    // ---- 2. mark -------------------------------------------------------
-    if (phases & kPhaseUnits) {
-      const uint32_t rot = (i_mid1 + lane) & 7;  // = table index & 7 of this lane's large primes
-      // absolute residue (q + rot) & 7 at step q: its plane and e bit
-      const uint32_t pl_rot = ((wa.pl_pack >> (3 * rot)) | (wa.pl_pack << (24 - 3 * rot))) & 0xFFFFFFu;
-      const uint32_t e_rot = ((wa.e_iota >> rot) | (wa.e_iota << (8 - rot))) & 0xFFu;
-      PlaneSteps ps;
-#pragma unroll
-      for (uint32_t q = 0; q < 8; ++q) {
-        ps.pb[q] = lds_addr(seg) + 32 * ((pl_rot >> (3 * q)) & 7u);
-        ps.ne[q] = 0u - ((e_rot >> q) & 1u);
+    const uint32_t img0 = lds_addr(img);
+    // bucketed hits of the primes > kWheelMaxPrime: one entry per marking
+    // thread (pipelined: the non-expander waves)
+    constexpr uint32_t kMarkT0 = DSE_PIPELINE ? NE * 64 : 0;
+    if (wa.bk_start && (phases & kPhaseLarge) && tid >= kMarkT0) {
+      const uint32_t b0 = wa.bk_start[s], b1 = wa.bk_start[s + 1];
+      for (uint32_t j = b0 + tid - kMarkT0; j < b1; j += NT - kMarkT0) {
+        const uint32_t e = wa.bk_entries[j];
+        mark_plane<false>(img0 + 32 * (e >> kWheelLogKP), e & (KP - 1));
       }
-      const uint64_t Kb = wa.KB0 + s * (uint64_t)KP;
-      // One dynamic queue over both lists, interleaved (list 1 at even, list 2
-      // at odd positions while both last). Claims run two units ahead: the LDS
-      // atomic for unit j+2 is issued when unit j starts and read when it ends
-      // (by then this wave's marks of unit j have drained), and a large unit's
-      // operands are loaded while the unit before it runs.
-      const uint32_t n_int = min(n1, n2), n_all = n1 + n2;
-      // The claim is an asm ds_add_rtn: written as a C++ atomic, the AMDGPU
-      // atomic optimizer aggregates it over the wave and waits for its return
-      // on the spot (draining the previous unit's marks with it), which
-      // defeats the two-ahead issue (+1% kernel time). Read through claimed().
-      const uint32_t ctr_addr = lds_addr(&lds.ctr);
-      auto claim = [&]() -> uint32_t {
-        uint32_t j = 0;
-        if (lane == 0) asm volatile("ds_add_rtn_u32 %0, %1, %2" : "=v"(j) : "v"(ctr_addr), "v"(1u) : "memory");
-        return j;  // per-lane value; lane 0 holds the claim
-      };
-      auto claimed = [&](uint32_t j) -> uint32_t {
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(j)::"memory");
-        return __builtin_amdgcn_readlane(j, 0);
-      };
-      auto is_l = [&](uint32_t u) -> bool { return u < 2 * n_int ? (u & 1) != 0 : n2 > n1; };
-      auto idx_of = [&](uint32_t u) -> uint32_t { return u < 2 * n_int ? u >> 1 : u - n_int; };
-      LargeOps cur, nxt;
-      uint32_t u_cur = claimed(claim());
-      uint32_t u_nxt = claimed(claim());
-      if (u_cur < n_all && is_l(u_cur)) load_L(cur, P, M, A, i_mid1 + 64 * idx_of(u_cur) + lane, i_big);
-      while (u_cur < n_all) {
-        const uint32_t c2 = claim();  // unit after next, read at the end of this one
-        if (u_nxt < n_all && is_l(u_nxt)) load_L(nxt, P, M, A, i_mid1 + 64 * idx_of(u_nxt) + lane, i_big);
-        const uint32_t k = idx_of(u_cur);
-        if (!is_l(u_cur)) {
-          if (k < nA) {
-            const uint32_t pi = __builtin_amdgcn_readfirstlane(s_mid_p[k]);
-            const uint32_t p = pi & 0xFFFFu;
-            const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mid_m[k] >> 32)) << 32) |
-                               (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_mid_m[k]);
-            if ((phases & kPhaseMidA) && (uint64_t)p * p < Vend) unit_A(seg, pi, m, Vs, wa.rho_pack, lane);
-          } else {
-            const uint32_t j0 = nA + (k - nA) * 8;
-            const uint32_t pf = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
-            if ((phases & kPhaseMidB) && (uint64_t)pf * pf < Vend)
-              unit_B(seg, s_mid_p, s_mid_m, j0, min(8u, n_mid - j0), Vs, Vend, wa.rho_pack, lane);
-          }
+    }
+    const uint32_t rot = (i_mid1 + lane) & 7;  // = table index & 7 of this lane's large primes
+    // absolute residue (q + rot) & 7 at step q: its plane and e bit
+    const uint32_t pl_rot = ((wa.pl_pack >> (3 * rot)) | (wa.pl_pack << (24 - 3 * rot))) & 0xFFFFFFu;
+    const uint32_t e_rot = ((wa.e_iota >> rot) | (wa.e_iota << (8 - rot))) & 0xFFu;
+    PlaneSteps ps;
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) {
+      ps.pb[q] = img0 + 32 * ((pl_rot >> (3 * q)) & 7u);
+      ps.ne[q] = 0u - ((e_rot >> q) & 1u);
+    }
+    const uint64_t Kb = wa.KB0 + s * (uint64_t)KP;
+    // One dynamic queue over both lists, interleaved (list 1 at even, list 2
+    // at odd positions while both last). Claims run two units ahead: the LDS
+    // atomic for unit j+2 is issued when unit j starts and read when it ends
+    // (by then this wave's marks of unit j have drained), and a large unit's
+    // operands are loaded while the unit before it runs.
+    const uint32_t n_int = min(n1, n2), n_all = n1 + n2;
+    // The claim is an asm ds_add_rtn: written as a C++ atomic, the AMDGPU
+    // atomic optimizer aggregates it over the wave and waits for its return
+    // on the spot (draining the previous unit's marks with it), which
+    // defeats the two-ahead issue. Read through claimed().
+    const uint32_t ctr_addr = lds_addr(&lds.ctr[ctr_i]);
+    auto claim = [&]() -> uint32_t {
+      uint32_t j = 0;
+      if (lane == 0) asm volatile("ds_add_rtn_u32 %0, %1, %2" : "=v"(j) : "v"(ctr_addr), "v"(1u) : "memory");
+      return j;  // per-lane value; lane 0 holds the claim
+    };
+    auto claimed = [&](uint32_t j) -> uint32_t {
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(j)::"memory");
+      return __builtin_amdgcn_readlane(j, 0);
+    };
+    auto is_l = [&](uint32_t u) -> bool { return u < 2 * n_int ? (u & 1) != 0 : n2 > n1; };
+    auto idx_of = [&](uint32_t u) -> uint32_t { return u < 2 * n_int ? u >> 1 : u - n_int; };
+    LargeOps cur, nxt;
+    uint32_t u_cur = claimed(claim());
+    uint32_t u_nxt = claimed(claim());
+    if (u_cur < n_all && is_l(u_cur)) load_L(cur, P, M, A, i_mid1 + 64 * idx_of(u_cur) + lane, i_big);
+    while (u_cur < n_all) {
+      const uint32_t c2 = claim();  // unit after next, read at the end of this one
+      if (u_nxt < n_all && is_l(u_nxt)) load_L(nxt, P, M, A, i_mid1 + 64 * idx_of(u_nxt) + lane, i_big);
+      const uint32_t k = idx_of(u_cur);
+      if (!is_l(u_cur)) {
+        if (k < nA) {
+          const uint32_t pi = __builtin_amdgcn_readfirstlane(s_mid_p[k]);
+          const uint32_t p = pi & 0xFFFFu;
+          const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mid_m[k] >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_mid_m[k]);
+          if ((phases & kPhaseMidA) && (uint64_t)p * p < Vend) unit_A(img, pi, m, Vs, wa.rho_pack, lane);
         } else {
-          const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p);
-          if ((phases & kPhaseLarge) && (uint64_t)p0 * p0 < Vend) unit_L(seg, cur, Vs, Vend, Kb, ps, pl_rot, wa.rho_pack);
+          const uint32_t j0 = nA + (k - nA) * 8;
+          const uint32_t pf = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
+          if ((phases & kPhaseMidB) && (uint64_t)pf * pf < Vend)
+            unit_B(img, s_mid_p, s_mid_m, j0, min(8u, n_mid - j0), Vs, Vend, wa.rho_pack, lane);
         }
-        cur = nxt;
-        u_cur = u_nxt;
-        u_nxt = claimed(c2);
+      } else {
+        const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p);
+        if ((phases & kPhaseLarge) && (uint64_t)p0 * p0 < Vend) unit_L(cur, Vs, Vend, Kb, ps, pl_rot, wa.rho_pack);
       }
-      // bucketed hits of the primes > kWheelMaxPrime: one entry per thread
-      if (wa.bk_start && (phases & kPhaseLarge)) {
-        const uint32_t b0 = wa.bk_start[s], b1 = wa.bk_start[s + 1];
-        const uint32_t lds0 = lds_addr(seg);
-        for (uint32_t j = b0 + tid; j < b1; j += NT) {
-          const uint32_t e = wa.bk_entries[j];
-          mark_plane<false>(lds0 + 32 * (e >> 17), e & (KP - 1));
-        }
-      }
+      cur = nxt;
+      u_cur = u_nxt;
+      u_nxt = claimed(c2);
     }
-    lds_drain();
-    DSE_TSTAMP(2);
-    __syncthreads();
-    DSE_TSTAMP(3);
+  };
 
-    // ---- 3. expand to odd-only bits, count, store ------------------------
-    if (phases & kPhaseExpand) {
-      const uint32_t c = lane >> 3, a8 = lane & 7;
-      const uint64_t seg_word0 = s * (uint64_t)kOutWordsPerSeg;
-#pragma unroll 1
-      for (uint32_t t = 0; t < ROWS / (NW * 8); ++t) {
-        const uint32_t row = 8 * ((ROWS / (NW * 8)) * wave + t) + a8;
-        const uint32_t* rp = seg + row * 64 + c;
-        uint32_t Q[8];
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) Q[j] = ~rp[8 * ((j + a8) & 7)];  // plane (j + a8) & 7, 1 = prime
-        // un-rotate by a8 (plane i = Q[(i - a8) & 7]): three conditional rotations
-        uint32_t R1[8], R2[8], Pw[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) R1[i] = (a8 & 1) ? Q[(i + 7) & 7] : Q[i];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) R2[i] = (a8 & 2) ? R1[(i + 6) & 7] : R1[i];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) Pw[i] = (a8 & 4) ? R2[(i + 4) & 7] : R2[i];
-        uint32_t TL[4], TH[4];
-        byte_transpose4(Pw, TL);
-        byte_transpose4(Pw + 4, TH);
-        uint32_t o[15];
-#pragma unroll
-        for (int w = 0; w < 15; ++w) o[w] = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint64_t x = transpose8((uint64_t)TL[q] | ((uint64_t)TH[q] << 32));
-#pragma unroll
-          for (int bb = 0; bb < 8; ++bb) {
-            const uint32_t e = s_lut[(uint32_t)(x >> (8 * bb)) & 0xFFu];
-            const int pos = 15 * (8 * q + bb);
-            o[pos >> 5] |= e << (pos & 31);
-            if ((pos & 31) > 17) o[(pos >> 5) + 1] |= e >> (32 - (pos & 31));
-          }
-        }
-        const uint64_t w0 = seg_word0 + 15ull * (c * ROWS + row);  // caller's 32-bit word index
-        if (s == 0 && c == 0 && row == 0) o[0] |= wa.fix0;
-        const uint64_t bit0 = 32ull * w0;
-        if (bit0 + 480 > wa.nbits) {  // range end (last segment only)
-          const uint32_t rem = bit0 >= wa.nbits ? 0u : (uint32_t)(wa.nbits - bit0);  // < 480 valid bits
-#pragma unroll
-          for (int w = 0; w < 15; ++w) {
-            const uint32_t b = 32u * w;
-            o[w] = b >= rem ? 0u : (rem - b >= 32 ? o[w] : o[w] & ((1u << (rem - b)) - 1u));
-          }
-        }
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int w = 0; w < 15; ++w) cnt += __popc(o[w]);
-        my_count += cnt;
-        if (out && (phases & kPhaseStore)) {
-          if (w0 + 15 <= out_words) {
-#pragma unroll
-            for (int w = 0; w < 15; ++w) out[w0 + w] = o[w];
-          } else {
-#pragma unroll
-            for (int w = 0; w < 15; ++w)
-              if (w0 + w < out_words) out[w0 + w] = o[w];
-          }
-        }
+#if DSE_PIPELINE
+  if (T > 0) {
+    if (expander) init_segment(lds.img[0], blockIdx.x);
+    __syncthreads();
+    // round t: image t&1 is marked (segment of round t), image (t+1)&1 holds
+    // the segment of round t-1 (expanded, then re-initialised for round t+1)
+    for (uint32_t t = 0; t <= T; ++t) {
+      const uint32_t X = t & 1;
+      const uint64_t s = blockIdx.x + (uint64_t)t * grid;
+      if (expander) {
+        if (t >= 1 && (phases & kPhaseExpand)) expand_segment(lds.img[X ^ 1], s - grid);
+        if (t + 1 < T) init_segment(lds.img[X ^ 1], s + grid);
+        if (tid == 0) lds.ctr[X ^ 1] = 0;  // round t+1's counter; its last claims were in round t-1
       }
+      if (t < T && (phases & kPhaseUnits)) mark_segment(lds.img[X], s, X);
+      lds_drain();
+      __syncthreads();
     }
+  }
+#else
+  if (T > 0) init_segment(lds.img[0], blockIdx.x);
+  __syncthreads();
+  for (uint32_t t = 0; t < T; ++t) {
+    const uint64_t s = blockIdx.x + (uint64_t)t * grid;
+    if (phases & kPhaseUnits) mark_segment(lds.img[0], s, 0);
+    lds_drain();
+    __syncthreads();
+    if (phases & kPhaseExpand) expand_segment(lds.img[0], s);
     // init of this workgroup's next segment, on the rows this wave just
     // expanded: no barrier in between, and waves drift into init while
-    // others still expand (-0.7%)
-    if (s + gridDim.x < nseg) init_segment(s + gridDim.x);
+    // others still expand
+    if (t + 1 < T) init_segment(lds.img[0], s + grid);
+    if (tid == 0) lds.ctr[0] = 0;  // all claims of this segment returned before the barrier above
     __syncthreads();
-    DSE_TSTAMP(4);
   }
+#endif
 
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) my_count += __shfl_xor(my_count, o);
-  if (lane_id == 0) s_wave_cnt[wave] = my_count;
+  if (lane_id == 0) lds.wave_cnt[wave] = my_count;
   __syncthreads();
   if (tid == 0) {
     unsigned long long t = 0;
-    for (uint32_t w = 0; w < NW; ++w) t += s_wave_cnt[w];
+    for (uint32_t w = 0; w < NW; ++w) t += lds.wave_cnt[w];
     if (t) atomicAdd(count_out, t);
   }
 }
@@ -891,10 +853,10 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
 
 // ---------------------------------------------------------------------------
 // Bucketed pass for the primes above kWheelMaxPrime (high-offset windows):
-// such a prime hits a 3.9 M-integer segment less than once, so instead of
+// such a prime hits a 2 M-integer segment less than once, so instead of
 // visiting every (prime, segment) pair the kernels below walk each prime's
 // multiples p*m, gcd(m, 30) = 1, across the whole range once and file every
-// hit under its segment: k | plane << 17. Two identical walks: count (LDS
+// hit under its segment: k | plane << 16. Two identical walks: count (LDS
 // per-segment counters -> per-workgroup column), then fill (LDS cursors
 // seeded from the scanned columns). The wheel kernel ORs its segment's list.
 // ---------------------------------------------------------------------------
@@ -947,11 +909,11 @@ __device__ __forceinline__ void bucket_walk(uint32_t p, uint64_t m, const Bucket
   uint32_t w3 = 3 * __popc(kCoprime30 & ((1u << (r30 + d)) - 1));  // 3 * index of (m mod 30) in R30
   uint64_t o = (uint64_t)p * (m0 + d) - ba.V0;
   while (o < ba.span) {
-    const uint32_t s = ((uint32_t)(o >> 17)) / 30u;  // o < 2^49
+    const uint32_t s = ((uint32_t)(o >> kWheelLogKP)) / 30u;  // o < 2^34
     const uint32_t u = (uint32_t)(o - (uint64_t)s * kWheelSpan);
     const uint32_t k = u / 30u, rho = u - 30u * k;
     const uint32_t pl = (uint32_t)(ba.plane_lut >> (3 * (rho >> 1))) & 7u;
-    emit(s, k | (pl << 17));
+    emit(s, k | (pl << kWheelLogKP));
     o += (uint64_t)p * ((kGap30 >> w3) & 7u);
     w3 = w3 == 21 ? 0u : w3 + 3;
   }
@@ -1039,23 +1001,33 @@ hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream) {
   return hipGetLastError();
 }
 
-#ifdef DSE_TIMING
-extern "C" int dse_debug_timing(unsigned long long* host) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(dse_timing), sizeof(dse_timing)) == hipSuccess ? 0 : -1;
+hipError_t free_scratch(Scratch* s) {
+  if (!s || !s->ptr) return hipSuccess;
+  hipError_t e = s->stream ? hipStreamSynchronize(s->stream) : hipSuccess;
+  const hipError_t f = hipFree(s->ptr);
+  s->ptr = nullptr;
+  s->bytes = 0;
+  s->stream = nullptr;
+  return e != hipSuccess ? e : f;
 }
-#endif
 
 namespace {
 
-// Launch geometry shared by the wheel kernel and the bucket walks.
-WheelArgs make_wheel_args(uint64_t g_start, uint64_t nbits, uint64_t* plane_lut) {
-  static const uint32_t phases = [] {
-    const char* e = getenv("DSE_PHASES");  // profiling-only ablation knob
-#ifndef DSE_PHASE_KNOB
-    if (e) fprintf(stderr, "dse: DSE_PHASES ignored: this libdse.so was built without -DDSE_PHASE_KNOB\n");
-#endif
+#ifdef DSE_PHASE_KNOB
+// Ablation builds only (tools/build_variant.sh knob -DDSE_PHASE_KNOB): the
+// DSE_PHASES bitmask switches kernel phases off. The production library reads
+// no environment variable.
+uint32_t knob_phases() {
+  static const uint32_t v = [] {
+    const char* e = getenv("DSE_PHASES");
     return e ? (uint32_t)strtoul(e, nullptr, 0) & kPhaseAll : kPhaseAll;
   }();
+  return v;
+}
+#endif
+
+// Launch geometry shared by the wheel kernel and the bucket walks.
+WheelArgs make_wheel_args(uint64_t g_start, uint64_t nbits, uint64_t* plane_lut) {
   WheelArgs wa{};
   const uint64_t v_start = 3 + 2 * g_start;
   wa.V0 = v_start - 1;
@@ -1080,8 +1052,11 @@ WheelArgs make_wheel_args(uint64_t g_start, uint64_t nbits, uint64_t* plane_lut)
   for (uint32_t v : small)
     if (v >= v_start && (v - v_start) / 2 < nbits) wa.fix0 |= 1u << ((v - v_start) / 2);
   for (int j = 0; j < kNQ; ++j) wa.v0q[j] = (uint8_t)(wa.V0 % kQ[j]);
-  for (int g = 0; g < kNG; ++g) wa.v0g[g] = (uint16_t)(wa.V0 % gmod(g));
-  wa.phases = phases;
+#ifdef DSE_PHASE_KNOB
+  wa.phases = knob_phases();
+#else
+  wa.phases = kPhaseAll;
+#endif
   return wa;
 }
 
@@ -1104,40 +1079,17 @@ uint64_t bucket_cap(uint64_t span, double a, double b) {
 
 constexpr uint64_t kBucketMaxEntries = 1ull << 31;  // 8 GB of entries per pass
 
-// Scratch for the bucket pass, one grow-only buffer per (device, stream): work
-// on one stream is ordered, so a buffer is never used by two passes at once,
-// while two contexts sieving windows concurrently on one device (different
-// streams) get separate buffers. Freed with the process.
-struct Scratch {
-  int dev;
-  hipStream_t stream;
-  void* ptr;
-  uint64_t bytes;
-};
-std::mutex g_scratch_mu;
-std::vector<Scratch> g_scratch;
-
-hipError_t bucket_scratch(uint64_t bytes, hipStream_t stream, char** out) {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  std::lock_guard<std::mutex> lock(g_scratch_mu);
-  Scratch* sc = nullptr;
-  for (Scratch& x : g_scratch)
-    if (x.dev == dev && x.stream == stream) sc = &x;
-  if (!sc) {
-    g_scratch.push_back(Scratch{dev, stream, nullptr, 0});
-    sc = &g_scratch.back();
-  }
+// Grow the context's scratch to `bytes` for a pass on `stream`.
+hipError_t ensure_scratch(Scratch* sc, uint64_t bytes, hipStream_t stream, char** out) {
+  hipError_t e;
+  // another stream's passes may still read the buffer
+  if (sc->ptr && sc->stream != stream && sc->stream && (e = hipStreamSynchronize(sc->stream)) != hipSuccess) return e;
   if (sc->bytes < bytes) {
-    // the stream's earlier passes may still read the old buffer
-    if (sc->ptr && ((e = hipStreamSynchronize(stream)) != hipSuccess || (e = hipFree(sc->ptr)) != hipSuccess))
-      return e;
-    sc->ptr = nullptr;
-    sc->bytes = 0;
+    if ((e = free_scratch(sc)) != hipSuccess) return e;
     if ((e = hipMalloc(&sc->ptr, bytes)) != hipSuccess) return e;
     sc->bytes = bytes;
   }
+  sc->stream = stream;
   *out = static_cast<char*>(sc->ptr);
   return hipSuccess;
 }
@@ -1152,8 +1104,9 @@ hipError_t launch_wheel(const void* table, const WheelArgs& wa, uint32_t* out, u
 
 }  // namespace
 
-hipError_t launch_sieve_range_wheel(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
-                                    unsigned long long* count, int num_cus, hipStream_t stream) {
+hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
+                              unsigned long long* count, int num_cus, hipStream_t stream, Scratch* scratch,
+                              const SieveOpts* opts) {
   if (nbits == 0) return hipSuccess;
   const uint64_t vmax = 3 + 2 * (g_start + nbits - 1);
   const uint64_t root = isqrt64(vmax);
@@ -1162,14 +1115,12 @@ hipError_t launch_sieve_range_wheel(const void* table, uint64_t g_start, uint64_
     const WheelArgs wa = make_wheel_args(g_start, nbits, &plane_lut);
     return launch_wheel(table, wa, out, count, num_cus, stream);
   }
+  if (!scratch) return hipErrorInvalidValue;
   // primes above kWheelMaxPrime: passes of <= kBucketMaxSegs segments, each
   // with its own bucket build, then the wheel kernel over the pass
   const uint64_t total_seg = (nbits + kWheelOutBits - 1) / kWheelOutBits;
   uint64_t max_segs = kBucketMaxSegs;
-  if (const char* e = getenv("DSE_BUCKET_PASS_SEGS")) {  // test-only: force small passes
-    const uint64_t v = strtoull(e, nullptr, 0);
-    if (v >= 1 && v < max_segs) max_segs = v;
-  }
+  if (opts && opts->bucket_pass_segs >= 1 && opts->bucket_pass_segs < max_segs) max_segs = opts->bucket_pass_segs;
   for (uint64_t s0 = 0; s0 < total_seg;) {
     uint64_t ns = std::min<uint64_t>(max_segs, total_seg - s0);
     while (ns > 1 && bucket_cap(ns * kWheelSpan, (double)kWheelMaxPrime, (double)root) > kBucketMaxEntries) ns /= 2;
@@ -1188,7 +1139,7 @@ hipError_t launch_sieve_range_wheel(const void* table, uint64_t g_start, uint64_
     const uint64_t o_cols = 256, o_tot = o_cols + 4ull * kBucketGrid * ns, o_start = o_tot + 4 * ns + 256,
                    o_ent = (o_start + 4 * (ns + 1) + 255) & ~255ull, bytes = o_ent + 4 * cap;
     char* sc = nullptr;
-    hipError_t e = bucket_scratch(bytes, stream, &sc);
+    hipError_t e = ensure_scratch(scratch, bytes, stream, &sc);
     if (e != hipSuccess) return e;
     uint32_t* range = reinterpret_cast<uint32_t*>(sc);
     uint32_t* cols = reinterpret_cast<uint32_t*>(sc + o_cols);
@@ -1211,19 +1162,6 @@ hipError_t launch_sieve_range_wheel(const void* table, uint64_t g_start, uint64_
     s0 += ns;
   }
   return hipSuccess;
-}
-
-// Kernel choice: the wheel kernel (with the bucketed pass above
-// kWheelMaxPrime); DSE_KERNEL=odd forces the round-1 odd-only kernel (A/B).
-hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
-                              unsigned long long* count, int num_cus, hipStream_t stream) {
-  if (nbits == 0) return hipSuccess;
-  static const bool odd = [] {
-    const char* e = getenv("DSE_KERNEL");  // profiling-only
-    return e && e[0] == 'o';
-  }();
-  return odd ? launch_sieve_range_odd(table, g_start, nbits, out, count, num_cus, stream)
-             : launch_sieve_range_wheel(table, g_start, nbits, out, count, num_cus, stream);
 }
 
 }  // namespace dse

@@ -51,6 +51,7 @@ SIGNATURES = {
     "dse_base_table_prime_bytes": (_u64, [_u64]),
     "dse_base_table_finish_dev_async": (_i32, [_vp, _u64, _vp, _u64, _vp]),
     "dse_sieve_range_dev_async": (_i32, [_vp, _vp, _u64, _u64, _vp, _vp, _vp]),
+    "dse_debug_set_option": (_i32, [_vp, _cp, _i64]),
 }
 
 _lib = None

@@ -98,6 +98,10 @@ class Context:
         check(lib().dse_sieve_window(self.ptr, lo, hi, ctypes.byref(cnt)), "dse_sieve_window")
         return cnt.value
 
+    def debug_set_option(self, name: str, value: int) -> None:
+        """Test-only knob of this context (include/dse.h dse_debug_set_option)."""
+        check(lib().dse_debug_set_option(self.ptr, name.encode(), int(value)), "dse_debug_set_option")
+
     # -- device-buffer entry points (torch tensors' data_ptr()) --------------
     def base_primes_dev_async(self, limit: int, table_ptr: int, table_bytes: int, stream_ptr: int = 0):
         check(lib().dse_base_primes_dev_async(self.ptr, limit, table_ptr, table_bytes, stream_ptr or None),

@@ -133,8 +133,13 @@ class LineChannel:
             self.q.put(self._EOF)
 
     def get_line(self, timeout: Optional[float] = None) -> Optional[str]:
-        """Next non-empty line, None at end of stream."""
-        line = self.q.get(timeout=timeout)
+        """Next non-empty line, None at end of stream. timeout=None waits
+        forever, as the reference does (core.clj:54, sieve.clj:156); a finite
+        timeout that expires raises RuntimeError."""
+        try:
+            line = self.q.get(timeout=timeout)
+        except queue.Empty:
+            raise RuntimeError(f"no protocol line from the peer within {timeout} s") from None
         if line is self._EOF:
             self.q.put(self._EOF)
             return None
@@ -194,9 +199,18 @@ def _out_path(out_dir: Optional[str], my_num: int) -> str:
 # ------------------------------------------------------------------ follower
 
 
+def _expect(ch: LineChannel, what: str, timeout_s: Optional[float]):
+    msg = ch.get(timeout_s)
+    if msg is None:
+        raise RuntimeError(f"lead closed the connection before sending {what}")
+    return msg
+
+
 def client_start(host: str, port: int, *, out_dir: Optional[str] = None, sieve_fn: Optional[SieveFn] = None,
-                 device: int = 0, timeout_s: float = 600.0, write_file: bool = True) -> S.Chunk:
-    """core.clj:181-205 client-start, speaking the reference protocol."""
+                 device: int = 0, timeout_s: Optional[float] = None, write_file: bool = True) -> S.Chunk:
+    """core.clj:181-205 client-start, speaking the reference protocol. Like
+    the reference, every protocol wait is unbounded by default (a reference
+    lead marking prime by prime can take hours); timeout_s bounds them."""
     close = None
     if sieve_fn is None:
         sieve_fn, close = gpu_sieve_fn(device)
@@ -204,9 +218,13 @@ def client_start(host: str, port: int, *, out_dir: Optional[str] = None, sieve_f
     ch = LineChannel(socket.create_connection((host, port), timeout=timeout_s))
     ch.sock.settimeout(None)
     try:
-        my_num = int(ch.get(timeout_s))                           # core.clj:188
-        bounds = [int(x) for x in ch.get(timeout_s)]              # core.clj:189 (mapv int ...)
-        chunk = S.gen_table(bounds)                               # core.clj:190
+        my_num = _expect(ch, "the machine number", timeout_s)   # core.clj:188
+        if not isinstance(my_num, int):
+            raise RuntimeError(f"expected the machine number, got {my_num!r}")
+        bounds = _expect(ch, "the chunk bounds", timeout_s)     # core.clj:189 (mapv int ...)
+        if not (isinstance(bounds, list) and len(bounds) == 2):
+            raise RuntimeError(f"expected [lo hi] bounds, got {bounds!r}")
+        chunk = S.gen_table([int(x) for x in bounds])           # core.clj:190
         start = ch.get(timeout_s)                                 # core.clj:192
         if not start:
             raise RuntimeError("lead closed before the start signal")
@@ -240,13 +258,15 @@ def client_start(host: str, port: int, *, out_dir: Optional[str] = None, sieve_f
 
 def lead_start(num_expected: int, num_primes: int, port: int, *, host: str = "0.0.0.0",
                out_dir: Optional[str] = None, sieve_fn: Optional[SieveFn] = None, device: int = 0,
-               timeout_s: float = 600.0, write_file: bool = True,
+               timeout_s: Optional[float] = None, write_file: bool = True,
                ready: Optional[threading.Event] = None) -> S.Chunk:
     """core.clj:136-179 lead-start, speaking the reference protocol: accept
     num_expected-1 followers, hand out numbers and bounds, lead with chunk 1,
     relay every follower line to the machines numbered above its sender,
     stop at the appoint from machine P. With P = 1 the reference waits
-    forever for an appoint that never comes; here the run ends."""
+    forever for an appoint that never comes; here the run ends. Every wait
+    (accept, the last appoint) is unbounded by default, as in the reference
+    (core.clj:113,165-166); timeout_s bounds them (tests)."""
     P, n = int(num_expected), int(num_primes)
     close = None
     if sieve_fn is None:
@@ -294,18 +314,22 @@ def lead_start(num_expected: int, num_primes: int, port: int, *, host: str = "0.
                 errors.append(e)
                 done.set()
 
+        _sieve_chunk(lead_chunk, sieve_fn)                         # sieve.clj:131-146 on the GPU
+        lines = prime_lines(1, lead_chunk)
+        # Chunk 1's lines reach every follower before any relayed line: the
+        # relay threads start only after this broadcast (lines that followers
+        # send meanwhile wait in their LineChannel queues), so machine 3 never
+        # sees machine 2's lines, or its appoint, ahead of machine 1's primes.
+        for c in conns:                                            # send-chan broadcast (core.clj:93)
+            c.send(lines)
         threads = [threading.Thread(target=relay, args=(c,), daemon=True) for c in conns]
         for t in threads:
             t.start()
-        _sieve_chunk(lead_chunk, sieve_fn)                         # sieve.clj:131-146 on the GPU
-        lines = prime_lines(1, lead_chunk)
-        for c in conns:                                            # send-chan broadcast (core.clj:93)
-            c.send(lines)
         if write_file:
             S.finish(lead_chunk, 1, path=_out_path(out_dir, 1))    # sieve.clj:150
         print("Waiting for other machines to finish...\n", flush=True)
         if not done.wait(timeout_s):
-            raise TimeoutError("no appoint from the last machine")
+            raise RuntimeError(f"no appoint from the last machine within {timeout_s} s")
         if errors:
             raise errors[0]
         print("Shutting down server...\n", flush=True)
@@ -323,17 +347,24 @@ def lead_start(num_expected: int, num_primes: int, port: int, *, host: str = "0.
 
 def main(argv=None) -> int:
     """-main (core.clj:207-212) over the reference wire: 3 args = lead
-    (num-comps num-primes port), 2 args = follower (host port)."""
+    (num-comps num-primes port), 2 args = follower (host port). Optional
+    --timeout SECONDS bounds every protocol wait (default: wait forever)."""
     import sys
     argv = list(sys.argv[1:] if argv is None else argv)
+    timeout_s = None
+    if "--timeout" in argv:
+        i = argv.index("--timeout")
+        timeout_s = float(argv[i + 1])
+        del argv[i:i + 2]
     if len(argv) == 3:
-        c = lead_start(int(argv[0]), int(argv[1]), int(argv[2]))
+        c = lead_start(int(argv[0]), int(argv[1]), int(argv[2]), timeout_s=timeout_s)
         print(f"machine 1: {c.n_primes} odd primes in [{c.lower}, {c.upper})", flush=True)
     elif len(argv) == 2:
-        c = client_start(argv[0], int(argv[1]))
+        c = client_start(argv[0], int(argv[1]), timeout_s=timeout_s)
         print(f"{c.n_primes} odd primes in [{c.lower}, {c.upper})", flush=True)
     else:
-        print("usage: lead: <num-comps> <num-primes> <port> | follower: <host> <port>", file=sys.stderr)
+        print("usage: lead: <num-comps> <num-primes> <port> | follower: <host> <port> [--timeout S]",
+              file=sys.stderr)
         return 2
     return 0
 

@@ -107,7 +107,9 @@ int32_t dse_copy_chunk_mask(dse_ctx *ctx, int32_t my_num, uint64_t *mask);
 
 /* Sieve the odd values in [lo, hi] (any 64-bit window, lo,hi odd or even;
  * "segment-only" mode outside the reference's chunk semantics). Counts
- * primes in [max(lo,3), hi] among odd values. */
+ * primes in [max(lo,3), hi] among odd values. With several devices: the base
+ * primes are built on device 0 and RCCL-broadcast (as in dse_sieve_all), each
+ * device sieves one contiguous slice, the counts are RCCL all-reduced. */
 int32_t dse_sieve_window(dse_ctx *ctx, uint64_t lo, uint64_t hi, uint64_t *count);
 
 /* sieve.clj:82-108 finish: write chunk my_num's primes to path, byte-exact
@@ -161,6 +163,15 @@ int32_t dse_base_table_finish_dev_async(dse_ctx *ctx, uint64_t limit, void *tabl
 int32_t dse_sieve_range_dev_async(dse_ctx *ctx, const void *table_dev, uint64_t g_start,
                                   uint64_t nbits, uint64_t *mask_dev, uint64_t *count_dev,
                                   void *stream);
+
+/* ---- Test-only ---------------------------------------------------------- */
+
+/* Set a test-only option of this context (the production library reads no
+ * environment variable; defaults are the production configuration):
+ *   "bucket_pass_segments" = k > 0: bucketed passes of at most k segments
+ *   (covers the multi-pass path on small windows); 0 = default.
+ * DSE_EINVAL for an unknown name or a value out of range. */
+int32_t dse_debug_set_option(dse_ctx *ctx, const char *name, int64_t value);
 
 #ifdef __cplusplus
 }

@@ -343,11 +343,40 @@ def test_bucket_threshold_window_vs_oracle(ctx, oracle):
     assert c == c_ref and np.array_equal(m, m_ref)
 
 
-def test_bucket_multi_pass_mask(ctx, oracle, monkeypatch):
-    """Passes of 3 segments (DSE_BUCKET_PASS_SEGS, test-only knob): the pass
-    boundaries, the per-pass bucket builds and the output offsets, bit-exact."""
-    monkeypatch.setenv("DSE_BUCKET_PASS_SEGS", "3")
-    g0, nb = (10**14 + 12345) // 2 * 1 + 7, 10 * 1966080 + 12345  # ragged start and end, 11 segments
-    m, c = ctx.sieve_odd_range(g0, nb)
+def test_bucket_multi_pass_mask(oracle):
+    """Passes of 3 segments (test-only context option bucket_pass_segments):
+    the pass boundaries, the per-pass bucket builds and the output offsets,
+    bit-exact."""
+    from mail_sieve_e import sieve as S
+    g0, nb = (10**14 + 12345) // 2 * 1 + 7, 20 * 983040 + 12345  # ragged start and end, 21 segments
     m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
+    with S.Context(num_gpus=1) as c3:
+        c3.debug_set_option("bucket_pass_segments", 3)
+        m, c = c3.sieve_odd_range(g0, nb)
     assert c == c_ref and np.array_equal(m, m_ref)
+
+
+def test_bucket_scratch_freed_with_context():
+    """Each context owns its bucketed-pass scratch and dse_destroy frees it:
+    creating and destroying contexts that sieve a 1e18 slice must not shrink
+    the device's free memory (grow-only global scratch)."""
+    import torch
+    from mail_sieve_e import sieve as S
+    lo = 10**18
+    def once():
+        with S.Context(num_gpus=1) as c:
+            c.sieve_window(lo, lo + 2 * 10**8)
+    once()
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info()
+    for _ in range(4):
+        once()
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info()
+    assert free1 >= free0 - (64 << 20), (free0, free1)
+
+
+def test_debug_option_rejects_unknown(ctx):
+    from mail_sieve_e import _dse
+    with pytest.raises(_dse.DseError):
+        ctx.debug_set_option("no_such_option", 1)

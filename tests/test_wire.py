@@ -215,3 +215,42 @@ def test_wire_lead_gpu(oracle, tmp_path):
 @pytest.mark.gpu
 def test_wire_follower_gpu(oracle, tmp_path):
     _mixed_ref_lead(oracle, tmp_path, None, n=400_000, P=3)
+
+
+def _silent_lead(port, behaviour):
+    """A lead that accepts one follower and then `behaviour(conn)`."""
+    srv = socket.create_server(("127.0.0.1", port))
+    def go():
+        c, _ = srv.accept()
+        try:
+            behaviour(c)
+        finally:
+            c.close()
+            srv.close()
+    t = threading.Thread(target=go, daemon=True)
+    t.start()
+    return t
+
+
+def test_wire_follower_finite_timeout_is_a_protocol_error(oracle):
+    """A finite timeout (tests only; the default waits forever like the
+    reference) ends in a RuntimeError naming the wait, not queue.Empty."""
+    port = _free_port()
+    t = _silent_lead(port, lambda c: time.sleep(3))
+    with pytest.raises(RuntimeError, match="within"):
+        wire.client_start("127.0.0.1", port, sieve_fn=_oracle_fn(oracle), timeout_s=0.5, write_file=False)
+    t.join(5)
+
+
+def test_wire_follower_eof_before_number(oracle):
+    port = _free_port()
+    t = _silent_lead(port, lambda c: None)  # closes at once
+    with pytest.raises(RuntimeError, match="machine number"):
+        wire.client_start("127.0.0.1", port, sieve_fn=_oracle_fn(oracle), write_file=False)
+    t.join(5)
+
+
+def test_wire_default_waits_are_unbounded():
+    import inspect
+    assert inspect.signature(wire.client_start).parameters["timeout_s"].default is None
+    assert inspect.signature(wire.lead_start).parameters["timeout_s"].default is None
