@@ -7,7 +7,16 @@ sieve.clj:15-34), with every rank's inputs already on its GPU:
   primes to the other ranks (mirrors the reference's prime broadcast,
   sieve.clj:139), which derive Barrett factors and wheel offsets -> each
   rank sieves its chunk into an odd-only bitmask in HBM + count -> the last rank
-  also sieves the dropped tail -> RCCL all-reduce of the counts.
+  also sieves the dropped tail -> RCCL all-reduce of the counts -> the counts
+  on the host.
+Timing: every step runs from the call to the counts on the
+host; the headline is the median over the K timed steps of the per-step
+maximum over ranks. The K steps are also bracketed by barrier + synchronize
+(ms_per_step_bracketed), and K launches are timed back to back without host
+round trips (ms_per_step_pipelined).
+--window: the high-offset window [1e18, 1e18+1e10] split over the ranks
+(BASELINE config 5): rank 0 builds the base primes <= 1e9 + 4, RCCL
+broadcast, every rank sieves one contiguous slice, RCCL all-reduce.
 Single GPU: `python bench.py`; N GPUs: torch.distributed.run --nproc-per-node N.
 Prints ONE JSON line on rank 0.
 """
@@ -16,6 +25,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import statistics
 import sys
 import time
 
@@ -32,7 +42,9 @@ from mail_sieve_e import sieve as S  # noqa: E402
 from mail_sieve_e import work  # noqa: E402
 
 METRIC = "sieved integers/sec at N=1e11, 1/2/4/8 MI355X; % of LDS/HBM roofline"
-KNOWN_PI = {10**9: 50847534, 3 * 10**9: 144449537, 10**10: 455052511, 10**11: 4118054813, 10**12: 37607912018}
+KNOWN_PI = {10**9: 50847534, 10**10: 455052511, 10**11: 4118054813, 10**12: 37607912018}
+WINDOW = (10**18, 10**18 + 10**10)
+WINDOW_COUNT = 241272176  # oracle fast_count_window, tests/golden/golden.json
 
 
 def parse():
@@ -42,38 +54,57 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", "--N", dest="n", type=float, default=1e11,
                     help="sieve limit N (default 1e11, the headline); spell it --N under torch.distributed.run")
+    ap.add_argument("--window", action="store_true", help="the [1e18, 1e18+1e10] window instead of [3, N]")
     ap.add_argument("--no-mask", action="store_true", help="count only (not the product path; diagnostics)")
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
-    ap.add_argument("--cpu-sample-n", type=float, default=3e9)
+    ap.add_argument("--cpu-max-n", type=float, default=1e8, help="largest N of the CPU baseline runs")
     return ap.parse_args()
 
 
-def cpu_baseline(sample_n: int) -> dict:
-    """Time the oracle's faithful single-thread restatement of sieve.clj on a
-    bounded sample (rank 0, N=1 only). Test infrastructure: reported only."""
+def cpu_baseline(max_n: int) -> dict:
+    """The reference's lead + followers on this host's cores (SURVEY.md 8(d)
+    fallback: no JVM in the image): oracle/dse_oracle.c ref_sieve_threaded,
+    P machine threads + machine 1's relay thread exchanging [mi ps p]
+    messages through in-process queues, at P = 2 and 3 on the README (1e4) and
+    Run Lead.bat (1e6) workloads and up to max_n. Test infrastructure:
+    reported only, never the measured path."""
     from oracle import oracle as o
     o.lib()
-    t = time.perf_counter()
-    _, _, counts, msgs = o.sieve(sample_n, 1)
-    dt = time.perf_counter() - t
-    assert o.pi_ref(counts) == KNOWN_PI.get(sample_n, o.pi_ref(counts))
-    return {"value": sample_n / dt, "unit": "integers/s", "cores": 1, "kind": "port",
-            "sample": f"N={sample_n:.0e}, P=1 chunk: oracle/dse_oracle.c ref_sieve (faithful C restatement of "
-                      f"sieve.clj's per-prime lead loop, {msgs} prime messages), {dt:.2f} s on 1 host core; "
-                      "the Clojure reference cannot run (no JVM in the image)"}
+    runs = []
+    ns = [n for n in (10**4, 10**6, 10**7, 10**8, 10**9) if n <= max_n]
+    for n in ns:
+        for P in (2, 3):
+            t = time.perf_counter()
+            _, _, counts, msgs = o.sieve_threaded(n, P, want_masks=False)
+            dt = time.perf_counter() - t
+            if n in KNOWN_PI:
+                tail_g, tail_n = o.tail_range(n, P)
+                _, ct = o.fast_sieve_range(tail_g, tail_n, want_mask=False) if tail_n else (None, 0)
+                assert o.pi_ref(counts) + ct == KNOWN_PI[n], (n, P)
+            runs.append({"N": n, "P": P, "threads": P + 1, "seconds": dt, "integers_per_s": n / dt,
+                         "prime_messages": int(msgs)})
+    head = max((r for r in runs if r["P"] == 3), key=lambda r: r["N"])
+    return {"value": head["integers_per_s"], "unit": "integers/s", "cores": head["threads"], "kind": "port",
+            "nproc": os.cpu_count(),
+            "sample": f"N={head['N']:.0e}, P=3: oracle/dse_oracle.c ref_sieve_threaded, the reference's lead + "
+                      f"2 followers as 3 machine threads + the relay thread, per-prime [mi ps p] messages through "
+                      f"in-process queues ({head['prime_messages']} messages), {head['seconds']:.2f} s; "
+                      "the Clojure reference cannot run (no JVM in the image)",
+            "runs": runs}
 
 
-def pmc_summary(N: int, P: int):
+def pmc_summary(N: int, P: int, window: bool):
     """Per-launch figures of the sieve kernel from the committed rocprofv3 PMC
     passes for this config (profiles/<round>/pmc_*_sieve_kernel.csv, N=1e11,
     P=1): HBM bytes = 2*FETCH_SIZE + WRITE_SIZE (KiB counters; MI355X_MICROARCH.md:
-    gfx950 FETCH_SIZE counts half of a wide coalesced read, WRITE_SIZE is exact),
-    and the VALU / LDS wave-instruction issue rates per CU per cycle
+    gfx950 FETCH_SIZE counts half of a wide coalesced read, WRITE_SIZE is exact);
+    VALU issue against the 2.0 wave-instructions per CU-cycle ceiling, LDS busy
+    (SQ_LDS_IDX_ACTIVE per CU-cycle) and the bank-conflict share of it
     (GRBM_GUI_ACTIVE is summed over the 8 XCDs)."""
     import collections
     import csv
     import glob
-    if (N, P) != (10**11, 1):
+    if window or (N, P) != (10**11, 1):
         return None
     for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")), reverse=True):
         try:
@@ -86,9 +117,11 @@ def pmc_summary(N: int, P: int):
             v = {k: sum(x) / len(x) for k, x in vals.items()}
             cyc = v["GRBM_GUI_ACTIVE"] / 8
             return {"traffic": (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024, "source": os.path.relpath(d, ROOT),
-                    "valu_issue_per_cu_cycle": v["SQ_INSTS_VALU"] / 256 / cyc,
-                    "lds_issue_per_cu_cycle": v["SQ_INSTS_LDS"] / 256 / cyc,
-                    "lds_conflict_cycle_share": v["SQ_LDS_BANK_CONFLICT"] / v["SQ_LDS_IDX_ACTIVE"]}
+                    "cycles": cyc,
+                    "valu_issue_per_cu_cycle": v["SQ_INSTS_VALU"] / work.NUM_CUS / cyc,
+                    "valu_frac": v["SQ_INSTS_VALU"] / work.NUM_CUS / cyc / work.VALU_PEAK_PER_CU_CYCLE,
+                    "lds_busy": v["SQ_LDS_IDX_ACTIVE"] / work.NUM_CUS / cyc,
+                    "lds_conflict_share": v["SQ_LDS_BANK_CONFLICT"] / v["SQ_LDS_IDX_ACTIVE"]}
         except (OSError, KeyError, ZeroDivisionError):
             continue
     return None
@@ -96,7 +129,6 @@ def pmc_summary(N: int, P: int):
 
 def main():
     a = parse()
-    N = int(a.n)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -112,24 +144,36 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    P = world  # one spread-work chunk per GPU
-    cs = (N - 1) // 2 // P
-    g0 = rank * cs
-    tail_g, tail_n = P * cs, (N - 1) // 2 - P * cs
+    P = world  # one spread-work chunk (or window slice) per GPU
+    if a.window:
+        lo, hi = WINDOW
+        N = hi - lo                                  # integers covered
+        g_all, nb_all = (lo + 1 - 3) // 2, (hi - 1 - (lo + 1)) // 2 + 1  # odd values lo+1 .. hi-1
+        part = (nb_all + P - 1) // P
+        g0, cs = g_all + min(nb_all, part * rank), min(nb_all, part * (rank + 1)) - min(nb_all, part * rank)
+        tail_g = tail_n = 0
+        limit = S.base_limit_for_range(g_all, nb_all)
+        with_mask = False
+    else:
+        N = int(a.n)
+        cs = (N - 1) // 2 // P
+        g0 = rank * cs
+        tail_g, tail_n = P * cs, (N - 1) // 2 - P * cs
+        limit = S.base_limit_for_range(0, P * cs + tail_n)
+        with_mask = not a.no_mask
     words = (cs + 63) // 64
 
     ctx = S.Context(device=local)
-    limit = S.base_limit_for_range(0, P * cs + tail_n)
     tbytes = S.base_table_bytes(limit)
     pbytes = S.base_table_prime_bytes(limit)  # the primes: all a broadcast needs to carry
     table = torch.empty(tbytes, dtype=torch.uint8, device=dev)
     counts = torch.zeros(2, dtype=torch.int64, device=dev)
-    mask = None if a.no_mask else torch.empty(words, dtype=torch.int64, device=dev)
+    mask = torch.empty(words, dtype=torch.int64, device=dev) if with_mask else None
     stream = torch.cuda.current_stream(dev)
     sp = stream.cuda_stream
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    kev = []  # (start, end) HIP events around each sieve launch, on the stream it runs on
 
-    def step(i=None):
+    def launch(timed=False):
         counts.zero_()
         if rank == 0:
             ctx.base_primes_dev_async(limit, table.data_ptr(), tbytes, sp)
@@ -137,82 +181,128 @@ def main():
             dist.broadcast(table[:pbytes], src=0)
             if rank != 0:
                 ctx.base_table_finish_dev_async(limit, table.data_ptr(), tbytes, sp)
-        if i is not None:
-            ev[i][0].record(stream)
+        if timed:
+            e = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            e[0].record(stream)
         ctx.sieve_range_dev_async(table.data_ptr(), g0, cs, mask.data_ptr() if mask is not None else 0,
                                   counts.data_ptr(), sp)
-        if i is not None:
-            ev[i][1].record(stream)
+        if timed:
+            e[1].record(stream)
+            kev.append(e)
         if rank == world - 1 and tail_n:
             ctx.sieve_range_dev_async(table.data_ptr(), tail_g, tail_n, 0, counts.data_ptr() + 8, sp)
         if world > 1:
             dist.all_reduce(counts)
 
+    def step(timed=False):
+        """call -> counts on the host"""
+        t = time.perf_counter()
+        launch(timed)
+        c = counts.cpu().tolist()
+        return time.perf_counter() - t, c
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
     for _ in range(a.warmup):
         step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    g0_ev, g1_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    barrier()
     t0 = time.perf_counter()
-    g0_ev.record(stream)
-    for i in range(a.steps):
-        step(i)
-    g1_ev.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    step_s = []
+    for _ in range(a.steps):
+        dt, c = step(timed=True)
+        step_s.append(dt)
+    barrier()
     t1 = time.perf_counter()
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    kern = sum(e0.elapsed_time(e1) for e0, e1 in ev) / a.steps / 1e3  # s per sieve launch
+    # back-to-back launches without host round trips (the r01 headline method)
+    barrier()
+    tp0 = time.perf_counter()
+    for _ in range(a.steps):
+        launch()
+    barrier()
+    tp1 = time.perf_counter()
+
+    step_t = torch.tensor(step_s + [t1 - t0, tp1 - tp0], dtype=torch.float64, device=dev)
+    kern = sum(e0.elapsed_time(e1) for e0, e1 in kev) / len(kev) / 1e3  # s per sieve launch
     kern_t = torch.tensor([kern], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+        dist.all_reduce(step_t, op=dist.ReduceOp.MAX)
         dist.all_reduce(kern_t, op=dist.ReduceOp.MAX)
-    c = counts.cpu().tolist()
-    pi_ref, pi_full = 1 + c[0], 1 + c[0] + c[1]
-    T = elapsed.item()
+    st = step_t.cpu().tolist()
+    med = statistics.median(st[:a.steps])
+    bracketed, pipelined = st[a.steps] / a.steps, st[a.steps + 1] / a.steps
+    if a.window:
+        pi_ref = pi_full = c[0]
+        verified = c[0] == WINDOW_COUNT
+    else:
+        pi_ref, pi_full = 1 + c[0], 1 + c[0] + c[1]
+        verified = KNOWN_PI.get(N) == pi_full if N in KNOWN_PI else None
     if rank == 0:
-        rf = work.roofline(g0, cs, kern_t.item())
-        pmc = pmc_summary(N, P) if not a.no_mask else None
+        ks = kern_t.item()
+        if a.window:
+            workload = f"window [1e18, 1e18+1e10] split into {P} slice(s), one per GPU (count only, segment-only)"
+            rf = None
+        else:
+            workload = (f"N={N:.0e} odd-only chunked sieve, P={P} spread-work chunks (one per GPU), mask resident "
+                        "in HBM" + (" [count-only diagnostic]" if a.no_mask else ""))
+            rf = work.roofline(g0, cs, ks)
+        pmc = pmc_summary(N, P, a.window) if with_mask else None
         out = {
             "metric": METRIC,
-            "value": N * a.steps / T,
+            "value": N / med,
             "unit": "integers/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
-            "ms_per_step": T / a.steps * 1e3,
+            "ms_per_step": med * 1e3,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "deterministic (sieve of [3, N]; no input data)",
-            "config": {"workload": f"N={N:.0e} odd-only chunked sieve, P={P} spread-work chunks (one per GPU), "
-                                   "mask resident in HBM" + (" [count-only diagnostic]" if a.no_mask else ""),
-                       "N": N, "P": P, "cs": cs, "mask_bytes_per_gpu": 0 if a.no_mask else words * 8,
+            "data": "deterministic (sieve of [3, N]; no input data)" if not a.window else
+                    "deterministic (the window's odd values; no input data)",
+            "config": {"workload": workload, "N": N, "P": P, "cs": cs,
+                       "mask_bytes_per_gpu": words * 8 if with_mask else 0,
                        "parallelism": f"range-partition x{P} (RCCL broadcast + all-reduce)"},
-            "ms_per_step_gpu": g0_ev.elapsed_time(g1_ev) / a.steps,
+            "timing": "median over steps of the per-step max over ranks, call -> counts on the host",
+            "ms_per_step_bracketed": bracketed * 1e3,
+            "ms_per_step_pipelined": pipelined * 1e3,
             "pi_ref": pi_ref,
             "pi_full": pi_full,
-            "verified": KNOWN_PI.get(N) == pi_full if N in KNOWN_PI else None,
-            "roofline": {"bound": rf["bound"],
-                         "achieved": rf["lds_achieved_gbs"] if rf["bound"] == "lds" else rf["hbm_achieved_gbs"],
-                         "peak": work.LDS_PEAK_GBS if rf["bound"] == "lds" else work.HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": rf["frac"], "traffic": pmc["traffic"] if pmc else None,
-                         "pmc_source": pmc["source"] if pmc else None,
-                         "wheel_marks_per_launch": rf["wheel_marks"], "frac_executed": rf["frac_executed"],
-                         "valu_issue_per_cu_cycle": pmc["valu_issue_per_cu_cycle"] if pmc else None,
-                         "lds_issue_per_cu_cycle": pmc["lds_issue_per_cu_cycle"] if pmc else None,
-                         "lds_conflict_cycle_share": pmc["lds_conflict_cycle_share"] if pmc else None,
-                         "kernel": "wheel_segments_kernel", "kernel_ms": kern_t.item() * 1e3,
-                         "marks_per_launch": rf["marks"], "bytes_per_mark": work.BYTES_PER_MARK,
-                         "hbm_bytes_per_launch": rf["hbm_bytes"], "hbm_achieved": rf["hbm_achieved_gbs"],
-                         "hbm_peak": work.HBM_PEAK_GBS},
+            "verified": verified,
+            "roofline": None,
             "cpu_baseline": None,
         }
-        if world == 1 and a.cpu_baseline == "on":
-            out["cpu_baseline"] = cpu_baseline(int(a.cpu_sample_n))
+        if rf is not None:
+            wm = rf["wheel_marks"]
+            achieved = work.LDS_OR_BYTES_PER_MARK * wm / ks / 1e9
+            out["roofline"] = {
+                "bound": "lds",
+                "achieved": achieved,
+                "peak": work.LDS_OR_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / work.LDS_OR_PEAK_GBS,
+                "traffic": pmc["traffic"] if pmc else None,
+                "basis": "executed ds_or_b32 marks (mod-30 wheel, primes > 61) x 4 B per kernel second against "
+                         "the LDS store path (64 B/clk/CU); kernel time from HIP events on the launch stream",
+                "kernel": "wheel_segments_kernel", "kernel_ms": ks * 1e3,
+                "executed_marks_per_launch": wm,
+                "frac_algorithmic": rf["frac"],
+                "algorithmic_marks_per_launch": rf["marks"],
+                "algorithmic_basis": "SURVEY 8(d): 8 B x odd-only marks from p^2 / 78.6 TB/s; the wheel executes "
+                                     f"{wm / rf['marks']:.3f} of them, so this exceeds 1",
+                "hbm_bytes_per_launch": rf["hbm_bytes"],
+                "hbm_frac": (pmc["traffic"] if pmc else rf["hbm_bytes"]) / ks / 1e9 / work.HBM_PEAK_GBS,
+                "valu_frac": pmc["valu_frac"] if pmc else None,
+                "valu_issue_per_cu_cycle": pmc["valu_issue_per_cu_cycle"] if pmc else None,
+                "lds_busy": pmc["lds_busy"] if pmc else None,
+                "lds_conflict_share": pmc["lds_conflict_share"] if pmc else None,
+                "pmc_source": pmc["source"] if pmc else None,
+            }
+        if world == 1 and a.cpu_baseline == "on" and not a.window:
+            out["cpu_baseline"] = cpu_baseline(int(a.cpu_max_n))
         print(json.dumps(out), flush=True)
     ctx.close()
     if world > 1:

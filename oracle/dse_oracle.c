@@ -14,20 +14,31 @@
  * the README's chunk size (README.txt:16) and the SURVEY.md section 4 table.
  * See DESIGN.md "Oracle".
  *
- * Two checkers live here:
+ * The checkers that live here:
  *   ref_*   a faithful, single-threaded restatement of sieve.clj: the same
  *           spread-work bounds, the same survivor scan with its end-of-chunk
  *           sentinel, the same per-prime lead/follower marking walk (including
  *           the early-indices skip), processed in the race-free order.
+ *   ref_sieve_threaded  the same machines as P threads exchanging [mi ps p]
+ *           messages through in-process queues, with machine 1's relay
+ *           (core.clj:118-134) as a thread of its own: the reference's
+ *           lead/follower run on one host's cores, timed by bench.py's
+ *           cpu_baseline leg (no JVM in the image).
  *   fast_*  an OpenMP odd-only segmented sieve used only to produce golden
  *           hashes at sizes the faithful restatement cannot reach; it is itself
  *           cross-checked against ref_* in tests/test_oracle.py.
+ *   fast_count_window  an independent OpenMP count of the primes in a high
+ *           window (outside the reference's semantics).
  */
 #include <math.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define REF_OK 0
 #define REF_EINVAL -1
@@ -269,5 +280,294 @@ int fast_sieve_range(uint64_t g0, uint64_t nbits, uint64_t *mask, uint64_t *coun
   }
   free(pr);
   if (count) *count = total;
+  return REF_OK;
+}
+
+/* ---------------------------------------------------------------------
+ * ref_sieve_threaded: the lead/follower run (core.clj:136-205,
+ * sieve.clj:118-172) as P machine threads plus machine 1's relay thread.
+ *   machine 1 leads first; for every survivor of its chunk it sends
+ *     [1 start prime] to every follower (send-chan broadcast,
+ *     core.clj:93-95), then marks its own chunk (sieve.clj:139-141);
+ *     at the end it sends the appoint [1 -1 0] to every follower (:148);
+ *   machine m >= 2 follows: it marks its chunk for every [mi ps p] it
+ *     receives (sieve.clj:156-164) until the appoint [m-1 -1 0], then leads,
+ *     sending its lines to the relay (its out-channel is the socket to
+ *     machine 1), which forwards each line to the machines > mi
+ *     (core.clj:122-126); the appoint from machine P ends the run (:132-134).
+ * FIFO queues give the race-free order of SURVEY.md section 5 (i), so the
+ * result equals ref_sieve's. Same outputs as ref_sieve.
+ * --------------------------------------------------------------------- */
+typedef struct {
+  int64_t mi, ps, p;
+} ref_msg;
+
+typedef struct {
+  ref_msg *buf;
+  size_t head, tail, cap;
+  pthread_mutex_t mu;
+  pthread_cond_t cv;
+} ref_queue;
+
+static int rq_init(ref_queue *q) {
+  q->cap = 1024;
+  q->head = q->tail = 0;
+  q->buf = (ref_msg *)malloc(q->cap * sizeof(ref_msg));
+  if (!q->buf) return REF_ENOMEM;
+  pthread_mutex_init(&q->mu, NULL);
+  pthread_cond_init(&q->cv, NULL);
+  return REF_OK;
+}
+
+static void rq_free(ref_queue *q) {
+  free(q->buf);
+  pthread_mutex_destroy(&q->mu);
+  pthread_cond_destroy(&q->cv);
+}
+
+static int rq_push(ref_queue *q, ref_msg m) {
+  pthread_mutex_lock(&q->mu);
+  if (q->tail == q->cap) {
+    if (q->head > 0) {
+      memmove(q->buf, q->buf + q->head, (q->tail - q->head) * sizeof(ref_msg));
+      q->tail -= q->head;
+      q->head = 0;
+    }
+    if (q->tail == q->cap) {
+      ref_msg *nb = (ref_msg *)realloc(q->buf, 2 * q->cap * sizeof(ref_msg));
+      if (!nb) { pthread_mutex_unlock(&q->mu); return REF_ENOMEM; }
+      q->buf = nb;
+      q->cap *= 2;
+    }
+  }
+  q->buf[q->tail++] = m;
+  pthread_cond_signal(&q->cv);
+  pthread_mutex_unlock(&q->mu);
+  return REF_OK;
+}
+
+static ref_msg rq_pop(ref_queue *q) {
+  pthread_mutex_lock(&q->mu);
+  while (q->head == q->tail) pthread_cond_wait(&q->cv, &q->mu);
+  ref_msg m = q->buf[q->head++];
+  pthread_mutex_unlock(&q->mu);
+  return m;
+}
+
+typedef struct ref_run ref_run;
+typedef struct {
+  ref_run *run;
+  int64_t my_num;
+} ref_machine;
+
+struct ref_run {
+  int64_t cs;
+  int32_t P;
+  uint8_t *flags;
+  ref_queue *q;   /* q[0] = relay (machine 1's transfer-primes), q[k-1] = machine k */
+  uint64_t nmsg;  /* prime messages (all leads) */
+  pthread_mutex_t nmsg_mu;
+  int err;
+};
+
+/* Lead phase of machine m (sieve.clj:131-150). */
+static void ref_lead(ref_run *r, int64_t m) {
+  const int64_t cs = r->cs;
+  uint8_t *own = r->flags + (size_t)(m - 1) * (size_t)cs;
+  uint64_t sent = 0;
+  int64_t start = ref_find_first_prime(own, cs);
+  for (;;) {
+    int64_t n_start = ref_find_next_non_zero(own, start, cs);
+    if (n_start < 0) break;
+    if (start >= cs || own[start] == 0) { r->err = REF_EINTERNAL; break; }
+    ref_msg msg = {m, start, 3 + 2 * ((m - 1) * cs + start)};
+    if (m == 1) {
+      for (int64_t k = 2; k <= r->P; ++k) rq_push(&r->q[k - 1], msg);
+    } else {
+      rq_push(&r->q[0], msg);
+    }
+    ++sent;
+    ref_mark_composites(m, cs, start, msg.p, m, own);
+    start = n_start;
+  }
+  ref_msg appoint = {m, -1, 0};
+  if (m == 1) {
+    for (int64_t k = 2; k <= r->P; ++k) rq_push(&r->q[k - 1], appoint);
+  } else {
+    rq_push(&r->q[0], appoint);
+  }
+  pthread_mutex_lock(&r->nmsg_mu);
+  r->nmsg += sent;
+  pthread_mutex_unlock(&r->nmsg_mu);
+}
+
+static void *ref_machine_main(void *arg) {
+  ref_machine *mc = (ref_machine *)arg;
+  ref_run *r = mc->run;
+  const int64_t m = mc->my_num;
+  uint8_t *own = r->flags + (size_t)(m - 1) * (size_t)r->cs;
+  if (m > 1) {
+    for (;;) { /* follower loop, sieve.clj:154-171 */
+      ref_msg msg = rq_pop(&r->q[m - 1]);
+      if (msg.ps == -1) {
+        if (msg.mi == m - 1) break; /* appointed */
+        continue;
+      }
+      ref_mark_composites(msg.mi, r->cs, msg.ps, msg.p, m, own);
+    }
+  }
+  ref_lead(r, m);
+  return NULL;
+}
+
+/* machine 1's transfer-primes handler (core.clj:118-134) */
+static void *ref_relay_main(void *arg) {
+  ref_run *r = (ref_run *)arg;
+  for (;;) {
+    ref_msg msg = rq_pop(&r->q[0]);
+    for (int64_t k = msg.mi + 1; k <= r->P; ++k) rq_push(&r->q[k - 1], msg);
+    if (msg.ps == -1 && msg.mi == r->P) break;
+  }
+  return NULL;
+}
+
+int ref_sieve_threaded(int64_t n, int32_t P, uint64_t *masks, uint64_t *counts, int64_t *cs_out,
+                       uint64_t *msgs) {
+  int64_t cs;
+  int rc = ref_spread_work(n, P, NULL, &cs);
+  if (rc) return rc;
+  if (cs_out) *cs_out = cs;
+  if (cs < 1) return REF_EINVAL;
+  ref_run r;
+  memset(&r, 0, sizeof(r));
+  r.cs = cs;
+  r.P = P;
+  r.flags = (uint8_t *)malloc((size_t)P * (size_t)cs);
+  r.q = (ref_queue *)calloc((size_t)P, sizeof(ref_queue));
+  ref_machine *mc = (ref_machine *)calloc((size_t)P, sizeof(ref_machine));
+  pthread_t *th = (pthread_t *)calloc((size_t)P + 1, sizeof(pthread_t));
+  if (!r.flags || !r.q || !mc || !th) { free(r.flags); free(r.q); free(mc); free(th); return REF_ENOMEM; }
+  memset(r.flags, 1, (size_t)P * (size_t)cs); /* gen-table */
+  pthread_mutex_init(&r.nmsg_mu, NULL);
+  for (int32_t k = 0; k < P; ++k) rq_init(&r.q[k]);
+  for (int32_t k = 0; k < P; ++k) {
+    mc[k].run = &r;
+    mc[k].my_num = k + 1;
+    pthread_create(&th[k], NULL, ref_machine_main, &mc[k]);
+  }
+  if (P > 1) pthread_create(&th[P], NULL, ref_relay_main, &r);
+  for (int32_t k = 0; k < P; ++k) pthread_join(th[k], NULL);
+  if (P > 1) pthread_join(th[P], NULL);
+  rc = r.err;
+  if (!rc) {
+    int64_t words = (cs + 63) / 64;
+    for (int32_t k = 0; k < P; ++k) {
+      uint64_t c = popcount_flags_to_mask(r.flags + (size_t)k * (size_t)cs, cs,
+                                          masks ? masks + (size_t)k * (size_t)words : NULL);
+      if (counts) counts[k] = c;
+    }
+    if (msgs) *msgs = r.nmsg;
+  }
+  for (int32_t k = 0; k < P; ++k) rq_free(&r.q[k]);
+  pthread_mutex_destroy(&r.nmsg_mu);
+  free(r.flags);
+  free(r.q);
+  free(mc);
+  free(th);
+  return rc;
+}
+
+/* ---------------------------------------------------------------------
+ * fast_count_window: number of primes among the odd values in [lo, hi]
+ * (lo >= 3), for high windows such as [1e18, 1e18 + 1e10] (SURVEY.md
+ * 8(a) a11). Independent of the GPU path: threads own contiguous slices of
+ * the window as plain bit arrays; primes below 2^22 are sieved in
+ * cache-sized segments with offsets carried from segment to segment, the
+ * larger ones (up to 1e9 for that window) mark their multiples directly.
+ * --------------------------------------------------------------------- */
+static uint64_t mulmod_u64(uint64_t a, uint64_t b, uint64_t m) {
+  return (uint64_t)(((unsigned __int128)a * b) % m);
+}
+
+/* first odd-index offset >= 0 (value a + 2*off) divisible by p, p odd, values
+ * a odd; the multiple must be >= p*p */
+static uint64_t first_off(uint64_t a, uint64_t p) {
+  uint64_t v = a;
+  uint64_t p2 = p * p;
+  if (v < p2) v = p2;
+  uint64_t r = v % p;
+  uint64_t w = r ? v + (p - r) : v;
+  if (!(w & 1)) w += p;
+  return (w - a) / 2;
+}
+
+int fast_count_window(uint64_t lo, uint64_t hi, uint64_t *count) {
+  if (!count) return REF_EINVAL;
+  *count = 0;
+  uint64_t a = lo < 3 ? 3 : lo;
+  if (!(a & 1)) ++a;
+  if (hi < a) return REF_OK;
+  uint64_t b = (hi & 1) ? hi : hi - 1;
+  uint64_t nb = (b - a) / 2 + 1; /* odd values a, a+2, ..., b */
+  uint64_t np;
+  uint32_t *pr = fast_base_primes(isqrt_u64(b), &np);
+  if (!pr) return REF_ENOMEM;
+  const uint64_t SMALL = 1ull << 22, SEG = 1ull << 21; /* bits */
+  uint64_t nsmall = 0;
+  while (nsmall < np && pr[nsmall] < SMALL) ++nsmall;
+  uint64_t total = 0;
+  int err = 0;
+  (void)mulmod_u64;
+#pragma omp parallel reduction(+ : total)
+  {
+    int nt = 1, t = 0;
+#ifdef _OPENMP
+    nt = omp_get_num_threads();
+    t = omp_get_thread_num();
+#endif
+    uint64_t per = (nb + (uint64_t)nt - 1) / (uint64_t)nt;
+    per = (per + 63) & ~63ull;
+    uint64_t s0 = per * (uint64_t)t, s1 = s0 + per < nb ? s0 + per : nb;
+    if (s0 < s1) {
+      uint64_t len = s1 - s0, words = (len + 63) / 64;
+      uint64_t *bits = (uint64_t *)calloc(words, 8); /* 1 = composite */
+      uint64_t *off = (uint64_t *)malloc((nsmall ? nsmall : 1) * 8);
+      if (!bits || !off) {
+#pragma omp atomic write
+        err = REF_ENOMEM;
+      } else {
+        const uint64_t va = a + 2 * s0; /* value of bit 0 */
+        for (uint64_t i = 0; i < nsmall; ++i) off[i] = first_off(va, pr[i]);
+        for (uint64_t g = 0; g < len; g += SEG) { /* small primes, segment by segment */
+          uint64_t ge = g + SEG < len ? g + SEG : len;
+          for (uint64_t i = 0; i < nsmall; ++i) {
+            uint64_t o = off[i], p = pr[i];
+            for (; o < ge; o += p) bits[o >> 6] |= 1ull << (o & 63);
+            off[i] = o;
+          }
+        }
+        for (uint64_t i = nsmall; i < np; ++i) { /* large primes: direct */
+          uint64_t p = pr[i];
+          if (p * p > va + 2 * (len - 1)) break;
+          for (uint64_t o = first_off(va, p); o < len; o += p) bits[o >> 6] |= 1ull << (o & 63);
+        }
+        uint64_t c = 0;
+        for (uint64_t w = 0; w < words; ++w) {
+          uint64_t v = ~bits[w];
+          if (w == words - 1 && (len & 63)) v &= (1ull << (len & 63)) - 1;
+          c += (uint64_t)__builtin_popcountll(v);
+        }
+        /* values that are small primes themselves (windows starting below
+         * sqrt(hi)): first_off starts at p*p, so p stays unmarked; 1 is not odd
+         * prime but a >= 3 excludes it */
+        total += c;
+      }
+      free(bits);
+      free(off);
+    }
+  }
+  free(pr);
+  if (err) return err;
+  *count = total;
   return REF_OK;
 }

@@ -39,7 +39,10 @@ def lib() -> ctypes.CDLL:
         L.ref_sieve_flags.argtypes = [i64, i32, ctypes.c_void_p, pu64]
         L.ref_finish.argtypes = [ctypes.c_char_p, i32, i64, i32, pu64]
         L.fast_sieve_range.argtypes = [u64, u64, pu64, pu64]
-        for f in (L.ref_spread_work, L.ref_sieve, L.ref_sieve_flags, L.ref_finish, L.fast_sieve_range):
+        L.ref_sieve_threaded.argtypes = [i64, i32, pu64, pu64, p64, pu64]
+        L.fast_count_window.argtypes = [u64, u64, pu64]
+        for f in (L.ref_spread_work, L.ref_sieve, L.ref_sieve_flags, L.ref_finish, L.fast_sieve_range,
+                  L.ref_sieve_threaded, L.fast_count_window):
             f.restype = ctypes.c_int
         _lib = L
     return _lib
@@ -81,6 +84,34 @@ def sieve(n: int, P: int):
     if rc:
         raise RuntimeError(f"ref_sieve rc={rc}")
     return cs, masks, counts, msgs.value
+
+
+def sieve_threaded(n: int, P: int, want_masks: bool = True):
+    """The lead/follower run as P machine threads + machine 1's relay thread,
+    exchanging [mi ps p] messages through in-process queues (the reference's
+    run on one host). Same results as sieve().
+
+    Returns (cs, masks[P, words] or None, counts[P], n_prime_messages)."""
+    cs, _ = spread_work(n, P)
+    if cs < 1:
+        raise ValueError("empty chunk")
+    masks = np.zeros((P, words_for(cs)), dtype=np.uint64) if want_masks else None
+    counts = np.zeros(P, dtype=np.uint64)
+    csv, msgs = ctypes.c_int64(), ctypes.c_uint64()
+    rc = lib().ref_sieve_threaded(n, P, _p(masks, ctypes.c_uint64), _p(counts, ctypes.c_uint64),
+                                  ctypes.byref(csv), ctypes.byref(msgs))
+    if rc:
+        raise RuntimeError(f"ref_sieve_threaded rc={rc}")
+    return cs, masks, counts, msgs.value
+
+
+def count_window(lo: int, hi: int) -> int:
+    """Independent OpenMP count of the primes among the odd values in [lo, hi]."""
+    cnt = ctypes.c_uint64()
+    rc = lib().fast_count_window(lo, hi, ctypes.byref(cnt))
+    if rc:
+        raise RuntimeError(f"fast_count_window rc={rc}")
+    return cnt.value
 
 
 def pi_ref(counts) -> int:

@@ -28,17 +28,42 @@ def _check_line(d: dict, n_gpus: int):
     for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
         assert k in rf, k
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-6 * rf["frac"] + 1e-12
+    assert 0 < rf["frac"] <= 1
+    # the headline is the median of per-step times, each from the call to the counts on the host
+    assert d["ms_per_step"] > 0 and d["ms_per_step_bracketed"] > 0 and d["ms_per_step_pipelined"] > 0
+    assert abs(d["value"] - d["config"]["N"] / (d["ms_per_step"] / 1e3)) < 1e-6 * d["value"]
 
 
 @pytest.mark.gpu
 def test_bench_single_gpu_line():
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--n", "1e10", "--steps", "2", "--warmup", "1",
-                        "--cpu-baseline", "on", "--cpu-sample-n", "1e8"],
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--n", "1e10", "--steps", "3", "--warmup", "1",
+                        "--cpu-baseline", "on", "--cpu-max-n", "1e7"],
                        capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     d = _last_json(r.stdout)
     _check_line(d, 1)
-    assert d["cpu_baseline"]["cores"] == 1 and d["cpu_baseline"]["value"] > 0
+    cb = d["cpu_baseline"]
+    # the reference's lead + 2 followers as threads + the relay thread (P = 3)
+    assert cb["cores"] == 4 and cb["value"] > 0 and cb["kind"] == "port"
+    assert {(x["N"], x["P"]) for x in cb["runs"]} == {(n, p) for n in (10**4, 10**6, 10**7) for p in (2, 3)}
+
+
+@pytest.mark.gpu
+def test_bench_window_two_rank_rehearsal():
+    """--window over 2 ranks on one GPU (gloo): table built on rank 0 and
+    broadcast, two slices, count all-reduced == the oracle's window count."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, DSE_BENCH_REHEARSE="1")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--window", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _last_json(r.stdout)
+    assert d["n_gpus"] == 2 and d["verified"] is True and d["pi_full"] == 241272176
+    assert d["config"]["P"] == 2 and d["value"] > 0
 
 
 @pytest.mark.gpu
