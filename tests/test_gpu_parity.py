@@ -112,18 +112,37 @@ def test_chunks_concatenate_to_single_chunk(ctx):
         assert not bk[cs:].any()  # tail bits of the last word are zero
 
 
+def _chunk_sha_streamed(ctx, N, P, k):
+    """SHA-256 of chunk k's resident mask (dse_copy_chunk_mask), hashed as it
+    is copied back."""
+    return sha(ctx.copy_chunk_mask(N, P, k))
+
+
 @pytest.mark.parametrize("P", [1, 2, 4, 8])
-def test_pi_1e11(ctx, P):
+def test_1e11_chunks_golden(ctx, P):
+    """The headline config, mask-level: every chunk's resident mask equals
+    the golden SHA-256 (tests/golden/make_golden.py --big11: the CPU fast
+    sieve, itself equal to the faithful restatement at 1e9 and 1e10)."""
+    g = GOLDEN["big"][f"1e11_P{P}"]
     counts, pi_ref, pi_full = ctx.sieve_all(10**11, P)
-    assert pi_ref == pi_full == 4_118_054_813
-    assert int(np.sum(counts)) + 1 == pi_ref
+    assert pi_ref == pi_full == 4_118_054_813 == g["pi_full"]
+    assert [int(x) for x in counts] == g["counts"]
+    for k in range(P):
+        assert _chunk_sha_streamed(ctx, 10**11, P, k + 1) == g["mask_sha256"][k], (P, k + 1)
 
 
 def test_pi_1e12_dropped_tail(ctx):
-    """SURVEY.md Gotcha 1: the reference's chunks lose 999999999989."""
+    """SURVEY.md Gotcha 1: the reference's chunks lose 999999999989. With the
+    golden 1e12 P=8 chunk hashes present (make_golden.py --big12), every
+    chunk's 7.8 GB mask is checked too."""
     counts, pi_ref, pi_full = ctx.sieve_all(10**12, 8)
     assert pi_ref == 37_607_912_017
     assert pi_full == 37_607_912_018
+    g = GOLDEN["big"].get("1e12_P8")
+    if g is not None:
+        assert [int(x) for x in counts] == g["counts"]
+        for k in range(8):
+            assert _chunk_sha_streamed(ctx, 10**12, 8, k + 1) == g["mask_sha256"][k], k + 1
 
 
 def test_idempotent(ctx):
@@ -254,11 +273,12 @@ def test_window_1e18_miller_rabin(ctx):
 
 def test_window_1e18_full(ctx):
     """BASELINE configs[4]: [1e18, 1e18+1e10]. No published count exists; the
-    value is pinned by additivity over sub-windows (plus the oracle and
-    Miller-Rabin checks above on slices of the same window)."""
+    golden value is the oracle's independent CPU count (fast_count_window,
+    make_golden.py --window), and additivity over sub-windows holds too."""
     total = ctx.sieve_window(10**18, 10**18 + 10**10)
+    assert total == GOLDEN["big"]["window_1e18"]["count"] == 241_272_176
     parts = sum(ctx.sieve_window(10**18 + k * 10**9 + (1 if k else 0), 10**18 + (k + 1) * 10**9) for k in range(10))
-    assert total == parts == 241_272_176
+    assert parts == total
 
 
 def test_window_two_contexts_concurrently(ctx):

@@ -148,3 +148,37 @@ def test_golden_big_constants():
     assert big["1e9_P1"]["pi_ref"] == 50_847_534
     for P in (2, 4, 8):
         assert big[f"1e10_P{P}"]["pi_ref"] == 455_052_511 == big[f"1e10_P{P}"]["pi_full"]
+
+
+@pytest.mark.parametrize("N,P", [(10_000, 2), (1_000_000, 3), (54_321, 7), (2_000_003, 8), (777, 1)])
+def test_threaded_run_equals_faithful(oracle, N, P):
+    """ref_sieve_threaded (P machine threads + the relay thread, in-process
+    queues; bench.py's cpu_baseline) reproduces ref_sieve bit for bit,
+    including the number of prime messages (1,228 / 78,497)."""
+    a = oracle.sieve(N, P)
+    b = oracle.sieve_threaded(N, P)
+    assert a[0] == b[0] and np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2]) and a[3] == b[3]
+
+
+@pytest.mark.parametrize("lo,hi", [(3, 10**6), (2, 2), (10**9, 10**9 + 10**6), (10**12 + 7, 10**12 + 3 * 10**6),
+                                   (10**15, 10**15 + 2 * 10**6), (999_999_999_989, 10**12)])
+def test_count_window_vs_fast_sieve(oracle, lo, hi):
+    """fast_count_window (the independent window counter behind the golden
+    [1e18, 1e18+1e10] count) agrees with the segmented fast sieve."""
+    a = max(lo, 3) | 1
+    b = hi if hi % 2 else hi - 1
+    want = 0 if b < a else oracle.fast_sieve_range((a - 3) // 2, (b - a) // 2 + 1, want_mask=False)[1]
+    assert oracle.count_window(lo, hi) == want
+
+
+def test_golden_streamed_headline_entries():
+    """1e11 P=1/2/4/8 (and, when generated, 1e12 P=8) golden chunk hashes:
+    counts add up to the published pi, chunk sizes follow spread-work."""
+    for P in (1, 2, 4, 8):
+        g = GOLDEN["big"][f"1e11_P{P}"]
+        assert g["cs"] == (10**11 - 1) // 2 // P and len(g["mask_sha256"]) == P
+        assert 1 + sum(g["counts"]) == g["pi_ref"] == g["pi_full"] == 4_118_054_813
+    g = GOLDEN["big"].get("1e12_P8")
+    if g is not None:
+        assert g["pi_ref"] == 37_607_912_017 and g["pi_full"] == 37_607_912_018
+    assert GOLDEN["big"]["window_1e18"]["count"] == 241_272_176
