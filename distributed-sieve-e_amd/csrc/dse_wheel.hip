@@ -73,11 +73,11 @@ constexpr uint32_t NE = DSE_NE;             // waves that expand and init
 static_assert(NE >= 1 && NE <= NW && (DSE_PIPELINE ? NE < NW : NE == NW) && ROWS % (8 * NE) == 0,
               "expander rows");
 #ifndef DSE_TA
-#define DSE_TA (LS / 16)
+#define DSE_TA 256
 #endif
 constexpr uint32_t TA = DSE_TA;             // A/B threshold
 #ifndef DSE_TB
-#define DSE_TB 8192
+#define DSE_TB 4096
 #endif
 constexpr uint32_t TB = DSE_TB;             // B/L threshold (<= LS)
 static_assert(TB <= LS && TB >= TA, "B/L threshold");
@@ -98,6 +98,41 @@ constexpr uint32_t inv30_const(uint32_t q) {
     if ((30 * x) % q == 1) return x;
   return 0;
 }
+// 30^{-1} mod q of the pattern primes, as constant tables: called in device
+// code outside a constant expression, inv30_const is not folded and runs its
+// search loop on the scalar unit at every call (it made the first init-table
+// builds 3.4x slower).
+constexpr uint32_t kQInv30[kNQ] = {inv30_const(7),  inv30_const(11), inv30_const(13), inv30_const(17),
+                                   inv30_const(19), inv30_const(23), inv30_const(29), inv30_const(31),
+                                   inv30_const(37), inv30_const(41), inv30_const(43), inv30_const(47),
+                                   inv30_const(53), inv30_const(59), inv30_const(61)};
+
+// Init tables: the 15 small primes in 7 groups G with period M_G = prod(G).
+// U_G[y] = 1 iff some q in G divides y. Plane i period k holds the value
+// Vs + rho_i + 30k, and q | Vs + rho_i + 30k <=> q | k + c_G with
+// c_G = (Vs + rho_i) * 30^{-1} mod M_G (gcd(30, M_G) = 1), so every plane
+// reads the same bit string at its own offset. A lane inits kInitRun
+// consecutive periods of one column: 33 dwords of each string from its bit
+// offset o, read as 9 aligned ds_read_b128 from the copy of the string that
+// is shifted by (o >> 5) & 3 dwords (4 copies), so every read is aligned
+// whatever o is; word r = alignbit(U[d0 + r + 1], U[d0 + r], o & 31).
+// DSE_INIT_REGS=1 keeps the round-1 register-shift init (A/B).
+#ifndef DSE_INIT_REGS
+#define DSE_INIT_REGS 0
+#endif
+constexpr int kNG = 7;
+constexpr uint32_t kGQ[kNG][3] = {{7, 11, 13}, {17, 19, 1}, {23, 29, 1}, {31, 37, 1},
+                                  {41, 43, 1}, {47, 53, 1}, {59, 61, 1}};
+constexpr uint32_t gmod(int g) { return kGQ[g][0] * kGQ[g][1] * kGQ[g][2]; }
+constexpr uint32_t kInitRun = 32 * (ROWS / NE);  // periods one lane inits per segment (one column)
+constexpr uint32_t kInitBlocks = kInitRun / 128 + 1;  // ds_read_b128 per lane and group
+// dwords per group string and copy: the reads reach dword d0 + 4 kInitBlocks - 1, d0 < M_G/32 + 1
+constexpr uint32_t gdw(int g) { return ((gmod(g) + 32 * (4 * kInitBlocks + 1) + 127) / 128) * 4; }
+constexpr uint32_t gbase(int g) { return g == 0 ? 0u : gbase(g - 1) + gdw(g - 1); }
+constexpr uint32_t kGDW = gbase(kNG);  // dwords per copy (620)
+constexpr uint32_t kGInv30[kNG] = {inv30_const(gmod(0)), inv30_const(gmod(1)), inv30_const(gmod(2)),
+                                   inv30_const(gmod(3)), inv30_const(gmod(4)), inv30_const(gmod(5)),
+                                   inv30_const(gmod(6))};
 
 struct WheelArgs {
   uint64_t V0;         // v_start - 1
@@ -109,6 +144,7 @@ struct WheelArgs {
   uint32_t fix0;       // output word 0 bits of the primes 3..61 inside the range
   uint32_t phases;
   uint8_t v0q[kNQ];    // V0 mod q
+  uint16_t v0g[kNG];   // V0 mod M_G (init tables)
   const uint32_t* bk_entries;  // bucketed hits of the primes > kWheelMaxPrime (or null):
   const uint32_t* bk_start;    // segment s owns entries [bk_start[s], bk_start[s+1]), k | plane << 16
 };
@@ -487,6 +523,9 @@ struct WheelLds {
   uint64_t mid_m[kMidCap];         // Barrett factors of the staged mid primes
   uint32_t mid_p[kMidCap];         // p | (30^{-1} mod p) << 16
   uint32_t lut[256];               // period byte -> 15 odd slots
+#if !DSE_INIT_REGS
+  uint4 itab[kGDW];                // init tables U_G, 4 copies shifted by 0..3 dwords (kGDW / 4 blocks each)
+#endif
   uint32_t thr[4];
   uint32_t ctr[2];                 // unit counters (pipelined: one per image)
   unsigned long long wave_cnt[NW];
@@ -546,6 +585,27 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     }
     s_lut[tid] = v;
   }
+#if !DSE_INIT_REGS
+  // copy k, group g, dword i = bits [32 (i + k), 32 (i + k) + 32) of U_g
+  for (uint32_t idx = tid; idx < 4 * kGDW; idx += NT) {
+    const uint32_t k = idx / kGDW, i = idx - k * kGDW;
+    uint32_t v = 0;
+#pragma unroll
+    for (int g = 0; g < kNG; ++g) {
+      if (i >= gbase(g) && i < gbase(g) + gdw(g)) {
+        const uint32_t y0 = 32 * (i - gbase(g) + k);
+#pragma unroll 1
+        for (uint32_t b = 0; b < 32; ++b) {
+          const uint32_t y = y0 + b;
+          bool hit = y % kGQ[g][0] == 0 || y % kGQ[g][1] == 0;
+          if (kGQ[g][2] > 1) hit = hit || y % kGQ[g][2] == 0;
+          v |= (uint32_t)hit << b;
+        }
+      }
+    }
+    reinterpret_cast<uint32_t*>(lds.itab)[idx] = v;
+  }
+#endif
   __syncthreads();
   const uint32_t i_mid0 = s_thr[0], i_midB = s_thr[1], i_mid1 = s_thr[2];
   for (uint32_t i = tid; i < i_mid1 - i_mid0; i += NT) {
@@ -582,6 +642,13 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     const uint32_t r0 = wave * (ROWS / NE);
     const uint32_t k0 = c * LS + 32 * r0;                // first period of the lane's words
     const bool on = phases & kPhaseSmall;
+#ifdef DSE_PHASE_KNOB
+    if (!on) {  // ablation: zero-fill only, no pattern arithmetic
+      for (uint32_t r = 0; r < ROWS / NE; ++r) img[(r0 + r) * 64 + C] = 0;
+      return;
+    }
+#endif
+#if DSE_INIT_REGS
     uint32_t res[kNQ];
 #pragma unroll
     for (int j = 0; j < kNQ; ++j) {
@@ -591,7 +658,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       const uint32_t sq = (uint32_t)(s % q);
       const uint32_t x = ((uint32_t)wa.v0q[j] + sq * wq + rho + (30u * k0) % q) % q;
       const uint32_t u = x ? q - x : 0u;
-      res[j] = (u * inv30_const(q)) % q;                 // first k >= k0 with q | value, minus k0
+      res[j] = (u * kQInv30[j]) % q;                     // first k >= k0 with q | value, minus k0
     }
 #pragma unroll 2
     for (uint32_t r = 0; r < ROWS / NE; r += 2) {
@@ -603,10 +670,51 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         w |= pat64(q) << res[j];
         res[j] = res[j] >= d ? res[j] - d : res[j] + q - d;
       }
-      if (!on) w = 0;
       img[(r0 + r) * 64 + C] = (uint32_t)w;
       img[(r0 + r + 1) * 64 + C] = (uint32_t)(w >> 32);
     }
+#else
+    constexpr uint32_t R = ROWS / NE;  // words per lane
+    constexpr uint32_t H = 16;         // words per pass (bounds the registers: 16 acc + 20 read)
+    static_assert(R % H == 0 && H % 4 == 0, "init passes");
+    uint32_t boff[kNG], bsh[kNG];      // per group: the lane's first aligned 16-byte block, bit shift
+    // rho takes 8 values over the lanes: left visible, the compiler evaluates
+    // the group offsets for all 8 on the scalar unit and selects per lane
+    // (a 6.8x SALU blow-up, 33 ms kernels); opaque, it is one VALU chain.
+    const uint32_t rho_o = opaque(rho), k0_o = opaque(k0);
+#pragma unroll
+    for (int g = 0; g < kNG; ++g) {
+      const uint32_t Mg = gmod(g);
+      const uint32_t wg = (uint32_t)(kWheelSpan % Mg);
+      const uint32_t sg = (uint32_t)(s % Mg);
+      const uint32_t x = ((uint32_t)wa.v0g[g] + sg * wg + rho_o) % Mg;  // (Vs + rho) mod M_G
+      const uint32_t o = (k0_o + x * kGInv30[g]) % Mg;                  // bit offset of period k0
+      const uint32_t d0 = o >> 5, kc = d0 & 3;
+      boff[g] = (kc * kGDW + gbase(g) + d0 - kc) / 4;                    // 16-byte block index
+      bsh[g] = o & 31;
+    }
+#pragma unroll
+    for (uint32_t h = 0; h < R; h += H) {
+      uint32_t acc[H];
+#pragma unroll
+      for (uint32_t r = 0; r < H; ++r) acc[r] = 0;
+#pragma unroll
+      for (int g = 0; g < kNG; ++g) {
+        const uint4* bp = lds.itab + boff[g] + h / 4;
+        uint32_t blk[H + 4];
+#pragma unroll
+        for (uint32_t b = 0; b < H / 4 + 1; ++b) {
+          const uint4 v = bp[b];
+          blk[4 * b] = v.x; blk[4 * b + 1] = v.y; blk[4 * b + 2] = v.z; blk[4 * b + 3] = v.w;
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < H; ++r) acc[r] |= __builtin_amdgcn_alignbit(blk[r + 1], blk[r], bsh[g]);
+        asm volatile("" ::: "memory");  // keep the next group's reads after these (register pressure)
+      }
+#pragma unroll
+      for (uint32_t r = 0; r < H; ++r) img[(r0 + h + r) * 64 + C] = acc[r];
+    }
+#endif
   };
 
   // ---- expand segment s (image img) to odd-only bits, count, store: lane
@@ -1052,6 +1160,7 @@ WheelArgs make_wheel_args(uint64_t g_start, uint64_t nbits, uint64_t* plane_lut)
   for (uint32_t v : small)
     if (v >= v_start && (v - v_start) / 2 < nbits) wa.fix0 |= 1u << ((v - v_start) / 2);
   for (int j = 0; j < kNQ; ++j) wa.v0q[j] = (uint8_t)(wa.V0 % kQ[j]);
+  for (int g = 0; g < kNG; ++g) wa.v0g[g] = (uint16_t)(wa.V0 % gmod(g));
 #ifdef DSE_PHASE_KNOB
   wa.phases = knob_phases();
 #else

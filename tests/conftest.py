@@ -9,6 +9,12 @@ for p in (ROOT, PKG_PARENT):
     if p not in sys.path:
         sys.path.insert(0, p)
 
+# Test harness only: DSE_TEST_LIB runs the suite against a variant build of
+# libdse.so (tools/build_variant.sh) before it replaces the production one.
+if os.environ.get("DSE_TEST_LIB"):
+    from mail_sieve_e import _dse as _d
+    _d.LIB_PATH = os.environ["DSE_TEST_LIB"]
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
