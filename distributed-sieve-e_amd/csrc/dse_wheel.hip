@@ -62,9 +62,6 @@ constexpr uint32_t NW = NT / 64;
 #ifndef DSE_PIPELINE
 #define DSE_PIPELINE 0
 #endif
-#ifndef DSE_L_EXEC
-#define DSE_L_EXEC 0
-#endif
 #ifndef DSE_NE
 #define DSE_NE (DSE_PIPELINE ? 8 : 16)
 #endif
@@ -446,6 +443,35 @@ struct PlaneSteps {
   uint32_t ne[8];
 };
 
+// Branch-free body of an L unit whose 64 primes are all live and past p^2
+// (the common case): the mark count per plane is decided once per unit.
+// MODE 2: pmin > KP, one predicated mark per plane; MODE 1: pmin > KP/2, two;
+// MODE 0: n_min unconditional marks per plane and a short loop for the rest.
+template <int MODE>
+__device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, const PlaneSteps& ps,
+                                            uint32_t n_min) {
+  const uint32_t p = o.p;
+#pragma unroll
+  for (uint32_t q = 0; q < 8; ++q) {
+    const uint32_t t = o.a[q] + nKbm + ps.ne[q];
+    uint32_t kk = min(t, t + p);  // plane start (a - Kb - e) mod p
+    const uint32_t pb32 = ps.pb[q];
+    if (MODE == 2) {
+      mark_plane<true>(pb32, kk);
+    } else if (MODE == 1) {
+      mark_plane<true>(pb32, kk);
+      mark_plane<true>(pb32, kk + p);
+    } else {
+#pragma unroll 2
+      for (uint32_t h = 0; h < n_min; ++h) {
+        mark_plane<false>(pb32, kk);
+        kk = opaque(kk + p);
+      }
+      for (; kk < KP; kk += p) mark_plane<false>(pb32, kk);  // a predicated fixed-count tail is slower
+    }
+  }
+}
+
 __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t Vend, uint64_t Kb,
                                        const PlaneSteps& ps, uint32_t pl_rot, uint64_t rho_pack) {
   const uint32_t p = o.p;
@@ -472,6 +498,12 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
   const uint32_t pmax = __builtin_amdgcn_readlane(p, 63);
   const bool none = __builtin_amdgcn_ballot_w64(!live || slow) != 0;
   const uint32_t n_min = (none || pmax >= KP) ? 0u : div_small(KP - pmax, pmax, fast_rcp((float)pmax));
+  if (!none) {  // every lane live and past p^2: branch-free bodies
+    if (pmin > KP) unit_L_fast<2>(o, nKbm, ps, 0);
+    else if (pmin > KP / 2) unit_L_fast<1>(o, nKbm, ps, 0);
+    else unit_L_fast<0>(o, nKbm, ps, n_min);
+    return;
+  }
   const uint32_t D = slow && live ? (uint32_t)(p2 - Vs) : 0u;
   if (!live) return;
   // Primes above KP/2 mark branch-free: a predicated-off mark is an OR of 0 at
@@ -493,27 +525,11 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
       }
     }
     const uint32_t pb32 = ps.pb[q];
-#if DSE_L_EXEC  // variant: exec-masked instead of predicated (OR 0) marks
-    if (pmin > KP) {
-      if (kk < KP) mark_plane<false>(pb32, kk);
-    } else if (pmin > KP / 2) {
-      if (kk < KP) mark_plane<false>(pb32, kk);
-      if (kk + p < KP) mark_plane<false>(pb32, kk + p);
-    } else {
-#else
-    if (pmin > KP) {
-      mark_plane<true>(pb32, kk);
-    } else if (pmin > KP / 2) {
+    if (pmin > KP / 2) {
       mark_plane<true>(pb32, kk);
       mark_plane<true>(pb32, kk + p);
     } else {
-#endif
-#pragma unroll 2
-      for (uint32_t h = 0; h < n_min; ++h) {
-        mark_plane<false>(pb32, kk);
-        kk = opaque(kk + p);
-      }
-      for (; kk < KP; kk += p) mark_plane<false>(pb32, kk);  // a predicated fixed-count tail is slower
+      for (; kk < KP; kk += p) mark_plane<false>(pb32, kk);
     }
   }
 }
