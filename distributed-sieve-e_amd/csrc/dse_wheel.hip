@@ -174,6 +174,48 @@ __device__ __forceinline__ void mark_col(uint32_t cb, uint32_t off) {
 
 __device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// Keeps a marking offset opaque to loop strength reduction, which otherwise
+// splits it into several induction variables (7 VALU per mark instead of 4).
+__device__ __forceinline__ uint32_t opaque(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// n unconditional marks off, off + p, ... in one column, unrolled by 4 by
+// hand (the asm marks keep the compiler from unrolling, which costs three
+// SALU of loop control per mark); returns the offset after the run.
+__device__ __forceinline__ uint32_t mark_run(uint32_t cb, uint32_t off, uint32_t p, uint32_t n) {
+  uint32_t h = 0;
+  for (; h + 4 <= n; h += 4) {
+    mark_col(cb, off);
+    mark_col(cb, opaque(off + p));
+    mark_col(cb, opaque(off + 2 * p));
+    mark_col(cb, opaque(off + 3 * p));
+    off = opaque(off + 4 * p);
+  }
+  for (; h < n; ++h) {
+    mark_col(cb, off);
+    off = opaque(off + p);
+  }
+  return off;
+}
+
+// Mark period `off` of the column at byte address cb if off < LS (else an OR
+// of 0 at a row inside the column); returns the offset of the next hit.
+__device__ __forceinline__ uint32_t mark_col_pred(uint32_t cb, uint32_t off, uint32_t p) {
+  const bool hit = off < LS;
+  const uint32_t bit = hit ? 1u << (off & 31) : 0u;
+  uint32_t a;
+  asm volatile(
+      "v_lshlrev_b32 %0, 3, %1\n\t"
+      "v_and_or_b32 %0, %0, %3, %2\n\t"
+      "ds_or_b32 %0, %4"
+      : "=&v"(a)
+      : "v"(off), "v"(cb), "s"((ROWS - 1) << 8), "v"(bit)
+      : "memory");
+  return hit ? off + p : off;
+}
+
 // x mod p for x < 2^63 with m = floor((2^64-1)/p).
 __host__ __device__ __forceinline__ uint32_t mod_barrett(uint64_t x, uint32_t p, uint64_t m) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -189,12 +231,6 @@ __host__ __device__ __forceinline__ uint32_t mod_barrett(uint64_t x, uint32_t p,
 
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
-// Keeps a marking offset opaque to loop strength reduction, which otherwise
-// splits it into several induction variables (7 VALU per mark instead of 4).
-__device__ __forceinline__ uint32_t opaque(uint32_t x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
 
 // t mod p, t < 2^24
 __device__ __forceinline__ uint32_t mod_small(uint32_t t, uint32_t p, float invp) {
@@ -264,25 +300,21 @@ __device__ __forceinline__ uint32_t kmin_for(uint32_t D, uint32_t rho) {
 }
 
 // 8 diagonal column steps of one lane's prime: per column n_u unconditional
-// marks and n_x value-predicated ones (wave-uniform counts, so the loop
-// control runs on the scalar unit); at the wrap from column 7 back to column 0
-// the offset restarts at the plane start O0.
+// marks and NX (template; NX < 0: n_x at run time) value-predicated ones
+// (wave-uniform counts, so the loop control runs on the scalar unit); at the
+// wrap from column 7 back to column 0 the offset restarts at the plane start O0.
+template <int NX>
 __device__ __forceinline__ void diag_walk(uint32_t* __restrict__ img, uint32_t off, uint32_t p, uint32_t cb,
                                           uint32_t c, uint32_t O0, uint32_t n_u, uint32_t n_x) {
   const uint32_t lds0 = lds_addr(img);
   for (uint32_t t = 0; t < 8; ++t) {
-    uint32_t* colp = img + cb + c;
     const uint32_t cb_col = lds0 + 4 * (cb + c);
-#pragma unroll 2
-    for (uint32_t h = 0; h < n_u; ++h) {
-      mark_col(cb_col, off);
-      off = opaque(off + p);
-    }
-    for (uint32_t h = 0; h < n_x; ++h) {
-      const bool hit = off < LS;
-      const uint32_t o = hit ? off : 0u;
-      lds_or(colp + ((o >> 5) << 6), hit ? 1u << (o & 31) : 0u);
-      off = hit ? off + p : off;
+    off = mark_run(cb_col, off, p, n_u);
+    if (NX >= 0) {
+#pragma unroll
+      for (int h = 0; h < NX; ++h) off = mark_col_pred(cb_col, off, p);
+    } else {
+      for (uint32_t h = 0; h < n_x; ++h) off = mark_col_pred(cb_col, off, p);
     }
     off -= LS;
     c = (c + 1) & 7;
@@ -335,11 +367,7 @@ __device__ __forceinline__ void unit_A(uint32_t* __restrict__ img, uint32_t pi, 
     const uint32_t cm = mod_small(c * LS, p, invp);
     uint32_t off = kp >= cm ? kp - cm : kp + p - cm;
     const uint32_t n_full = div_small(LS, p, invp);
-#pragma unroll 4
-    for (uint32_t h = 0; h < n_full; ++h) {
-      mark_col(cb_col, off);
-      off = opaque(off + p);
-    }
+    off = mark_run(cb_col, off, p, n_full);
     if (off < LS) mark_col(cb_col, off);
   } else {
     const uint32_t kmin = kmin_for((uint32_t)(p2 - Vs), rho);
@@ -387,7 +415,9 @@ __device__ __forceinline__ void unit_B(uint32_t* __restrict__ img, const uint32_
   // lanes past the batch end mark nothing (their unconditional marks would
   // land in another prime's columns)
   if (!valid) return;
-  diag_walk(img, off, p, cb, jp, O0, n_u, n_x);
+  if (n_x == 1) diag_walk<1>(img, off, p, cb, jp, O0, n_u, 1);
+  else if (n_x == 2) diag_walk<2>(img, off, p, cb, jp, O0, n_u, 2);
+  else diag_walk<-1>(img, off, p, cb, jp, O0, n_u, n_x);
 }
 
 // Operands of one large unit, loaded ahead of use. The table row of prime i
@@ -462,8 +492,13 @@ __device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, co
       mark_plane<true>(pb32, kk);
       mark_plane<true>(pb32, kk + p);
     } else {
-#pragma unroll 2
-      for (uint32_t h = 0; h < n_min; ++h) {
+      uint32_t h = 0;
+      for (; h + 2 <= n_min; h += 2) {  // unrolled by hand (asm marks)
+        mark_plane<false>(pb32, kk);
+        mark_plane<false>(pb32, opaque(kk + p));
+        kk = opaque(kk + 2 * p);
+      }
+      if (h < n_min) {
         mark_plane<false>(pb32, kk);
         kk = opaque(kk + p);
       }
