@@ -1,8 +1,9 @@
 #!/bin/bash
 # Build an A/B variant of libdse.so with extra defines: build_variant.sh NAME -DFOO=1 ...
+# tools/build_rev.sh builds one from a git revision.
 set -e
 NAME=$1; shift
-D=$(cd "$(dirname "$0")/../distributed-sieve-e_amd/csrc" && pwd)
+D=${SRC_DIR:-$(cd "$(dirname "$0")/../distributed-sieve-e_amd/csrc" && pwd)}  # SRC_DIR: another source tree (e.g. a git revision)
 OUT=$(cd "$(dirname "$0")/.." && pwd)/variants
 mkdir -p $OUT /tmp/dse_var_$NAME
 H="/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 $*"
