@@ -325,31 +325,33 @@ __device__ __forceinline__ void diag_walk(uint32_t off, uint32_t p, uint32_t pb,
   }
 }
 
-// 8x8 bit-matrix transpose: byte i bit j <-> byte j bit i.
-__device__ __forceinline__ uint64_t transpose8(uint64_t x) {
-  uint64_t t;
-  t = (x ^ (x >> 7)) & 0x00AA00AA00AA00AAull;
-  x ^= t ^ (t << 7);
-  t = (x ^ (x >> 14)) & 0x0000CCCC0000CCCCull;
-  x ^= t ^ (t << 14);
-  t = (x ^ (x >> 28)) & 0x00000000F0F0F0F0ull;
-  x ^= t ^ (t << 28);
-  return x;
+// (x & m) | (y & ~m): v_bfi_b32
+// (the compiler rewrites the C form into v_and + v_bitop3 pairs)
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t x, uint32_t y) {
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(x), "v"(y));
+  return r;
 }
 
-// v_perm_b32: byte n of the result = byte sel[n] of {hi:lo} (0-3 lo, 4-7 hi).
-__device__ __forceinline__ uint32_t perm(uint32_t hi, uint32_t lo, uint32_t sel) {
-  return __builtin_amdgcn_perm(hi, lo, sel);
+// Transpose the 8 x 8 bit matrix in each byte column q of W[0..7] (row i =
+// W[i] byte q): afterwards W[j] byte q bit i = old W[i] byte q bit j. Three
+// rounds of block swaps between rows i and i + s (blocks of s bits), 4 VALU
+// per swap: the upper s bits of row i's blocks trade places with the lower s
+// bits of row i + s's.
+template <int S>
+__device__ __forceinline__ void bit_block_swap(uint32_t& a, uint32_t& b) {
+  constexpr uint32_t m = S == 4 ? 0x0F0F0F0Fu : S == 2 ? 0x33333333u : 0x55555555u;
+  const uint32_t x = a, y = b;
+  b = bfi(m, x >> S, y);
+  a = bfi(~m, y << S, x);
 }
-
-// 4x4 byte transpose: T[q] byte i = P[i] byte q.
-__device__ __forceinline__ void byte_transpose4(const uint32_t* P, uint32_t* T) {
-  const uint32_t u0 = perm(P[1], P[0], 0x06020400u), u1 = perm(P[1], P[0], 0x07030501u);
-  const uint32_t v0 = perm(P[3], P[2], 0x06020400u), v1 = perm(P[3], P[2], 0x07030501u);
-  T[0] = perm(v0, u0, 0x05040100u);
-  T[2] = perm(v0, u0, 0x07060302u);
-  T[1] = perm(v1, u1, 0x05040100u);
-  T[3] = perm(v1, u1, 0x07060302u);
+__device__ __forceinline__ void bit_block_swaps(uint32_t (&W)[8]) {
+  bit_block_swap<4>(W[0], W[4]); bit_block_swap<4>(W[1], W[5]);
+  bit_block_swap<4>(W[2], W[6]); bit_block_swap<4>(W[3], W[7]);
+  bit_block_swap<2>(W[0], W[2]); bit_block_swap<2>(W[1], W[3]);
+  bit_block_swap<2>(W[4], W[6]); bit_block_swap<2>(W[5], W[7]);
+  bit_block_swap<1>(W[0], W[1]); bit_block_swap<1>(W[2], W[3]);
+  bit_block_swap<1>(W[4], W[5]); bit_block_swap<1>(W[6], W[7]);
 }
 
 // ---- work units of the mark phase ----------------------------------------
@@ -637,7 +639,9 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       const uint32_t rho = (uint32_t)(wa.rho_pack >> (5 * i)) & 31u;
       if (!(tid & (1u << i))) v |= 1u << ((rho - 1) >> 1);  // plane bit i clear: prime
     }
-    s_lut[tid] = v;  // composite bits of the 8 planes -> prime odd slots of the period
+    // composite bits of the 8 planes -> prime odd slots of the period, filed
+    // under lut_index(tid) (see there)
+    s_lut[tid ^ (3u * (tid >> 5))] = v;
   }
 #if !DSE_INIT_REGS
   // copy k, group g, dword i = bits [32 (i + k), 32 (i + k) + 32) of U_g
@@ -794,20 +798,27 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       const uint4* rp = reinterpret_cast<const uint4*>(img + row * 64 + 8 * c);
       const uint4 ra = rp[odd ? 1 : 0], rb = rp[odd ? 0 : 1];
       const uint4 lo = odd ? rb : ra, hi = odd ? ra : rb;
-      const uint32_t Pw[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};  // composite bits of planes 0..7
-      uint32_t TL[4], TH[4];
-      byte_transpose4(Pw, TL);
-      byte_transpose4(Pw + 4, TH);
+      uint32_t W[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};  // composite bits of planes 0..7
+      // Transpose every byte column of the 8 x 32 bit matrix in place (rows =
+      // planes): afterwards W[j] byte q bit i = plane i, period 8q + j.
+      bit_block_swaps(W);
+      // LUT index of every period byte v: v ^ 3 (v >> 5), a bijection that
+      // puts the common bytes (all composite, one prime) in distinct banks
+      // (indexed by v, 255 / 223 / 191 / 127 would share bank 31)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const uint32_t h = (W[j] >> 5) & 0x07070707u;
+        W[j] ^= h + (h << 1);  // 3h <= 21: no carry into the next byte
+      }
       uint32_t o[15];
 #pragma unroll
       for (int w = 0; w < 15; ++w) o[w] = 0;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const uint64_t x = transpose8((uint64_t)TL[q] | ((uint64_t)TH[q] << 32));
 #pragma unroll
-        for (int bb = 0; bb < 8; ++bb) {
-          const uint32_t e = s_lut[(uint32_t)(x >> (8 * bb)) & 0xFFu];
-          const int pos = 15 * (8 * q + bb);
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t e = s_lut[(W[j] >> (8 * q)) & 0xFFu];
+          const int pos = 15 * (8 * q + j);
           o[pos >> 5] |= e << (pos & 31);
           if ((pos & 31) > 17) o[(pos >> 5) + 1] |= e >> (32 - (pos & 31));
         }
@@ -815,23 +826,26 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       const uint64_t w0 = seg_word0 + 15ull * (c * ROWS + row);  // caller's 32-bit word index
       if (s == 0 && c == 0 && row == 0) o[0] |= wa.fix0;
       const uint64_t bit0 = 32ull * w0;
-      if (bit0 + 480 > wa.nbits) {  // range end (last segment only)
+      if (bit0 + 480 <= wa.nbits) {  // whole row inside the range (a separate path: no phi copies of o[])
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int w = 0; w < 15; ++w) cnt += __popc(o[w]);
+        my_count += cnt;
+        if (out && (phases & kPhaseStore)) {
+#pragma unroll
+          for (int w = 0; w < 15; ++w) out[w0 + w] = o[w];
+        }
+      } else {  // range end (last segment only): mask, count, store what is inside the caller's words
         const uint32_t rem = bit0 >= wa.nbits ? 0u : (uint32_t)(wa.nbits - bit0);  // < 480 valid bits
+        uint32_t cnt = 0;
 #pragma unroll
         for (int w = 0; w < 15; ++w) {
           const uint32_t b = 32u * w;
           o[w] = b >= rem ? 0u : (rem - b >= 32 ? o[w] : o[w] & ((1u << (rem - b)) - 1u));
+          cnt += __popc(o[w]);
         }
-      }
-      uint32_t cnt = 0;
-#pragma unroll
-      for (int w = 0; w < 15; ++w) cnt += __popc(o[w]);
-      my_count += cnt;
-      if (out && (phases & kPhaseStore)) {
-        if (w0 + 15 <= out_words) {
-#pragma unroll
-          for (int w = 0; w < 15; ++w) out[w0 + w] = o[w];
-        } else {
+        my_count += cnt;
+        if (out && (phases & kPhaseStore)) {
 #pragma unroll
           for (int w = 0; w < 15; ++w)
             if (w0 + w < out_words) out[w0 + w] = o[w];
