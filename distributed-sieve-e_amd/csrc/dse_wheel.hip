@@ -184,22 +184,34 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x) {
   return x;
 }
 
+// Mark period `off` of the column at cb and advance off by p, in one asm
+// block (written as mark_col + an add, the loop-carried offset costs a
+// v_mov per mark).
+__device__ __forceinline__ void mark_col_step(uint32_t cb, uint32_t& off, uint32_t p) {
+  uint32_t a, b;
+  asm volatile(
+      "v_lshlrev_b32 %0, 3, %2\n\t"
+      "v_and_or_b32 %0, %0, %4, %3\n\t"
+      "v_lshlrev_b32 %1, %2, 1\n\t"
+      "ds_or_b32 %0, %1\n\t"
+      "v_add_u32 %2, %2, %5"
+      : "=&v"(a), "=&v"(b), "+v"(off)
+      : "v"(cb), "s"(0xffffff00u), "v"(p)
+      : "memory");
+}
+
 // n unconditional marks off, off + p, ... in one column, unrolled by 4 by
 // hand (the asm marks keep the compiler from unrolling, which costs three
 // SALU of loop control per mark); returns the offset after the run.
 __device__ __forceinline__ uint32_t mark_run(uint32_t cb, uint32_t off, uint32_t p, uint32_t n) {
   uint32_t h = 0;
   for (; h + 4 <= n; h += 4) {
-    mark_col(cb, off);
-    mark_col(cb, opaque(off + p));
-    mark_col(cb, opaque(off + 2 * p));
-    mark_col(cb, opaque(off + 3 * p));
-    off = opaque(off + 4 * p);
+    mark_col_step(cb, off, p);
+    mark_col_step(cb, off, p);
+    mark_col_step(cb, off, p);
+    mark_col_step(cb, off, p);
   }
-  for (; h < n; ++h) {
-    mark_col(cb, off);
-    off = opaque(off + p);
-  }
+  for (; h < n; ++h) mark_col_step(cb, off, p);
   return off;
 }
 
@@ -356,6 +368,48 @@ __device__ __forceinline__ void bit_block_swaps(uint32_t (&W)[8]) {
 
 // ---- work units of the mark phase ----------------------------------------
 
+// ds_or_b32 at a precomputed LDS byte address (asm: see mark_col).
+__device__ __forceinline__ void mark_at(uint32_t a, uint32_t bit) {
+  asm volatile("ds_or_b32 %0, %1" : : "v"(a), "v"(bit) : "memory");
+}
+
+// A primes below TA_CLS, one column per lane, by residue class of the hit
+// index mod 32: hits n0, n0 + 32, n0 + 64, ... of a column share their bit
+// and sit p rows apart, so after 4 VALU of class setup each further mark is
+// one v_add of the wave-uniform 256 p (instead of 4 VALU per mark). Every
+// class has K = ROWS / p or K + 1 hits (its first row is < p): K marks, then
+// one predicated by row < ROWS, whose address is folded back into the image
+// (an OR of 0 there). off = first hit in the column (< p), img0 = image base
+// (aligned to the image size).
+#ifndef DSE_TA_CLS
+#define DSE_TA_CLS 224
+#endif
+constexpr uint32_t TA_CLS = DSE_TA_CLS;
+constexpr uint32_t IMG_BYTES = IMG_WORDS * 4;
+static_assert((IMG_BYTES & (IMG_BYTES - 1)) == 0, "image size is a power of two");
+template <int K>
+__device__ __forceinline__ void a_classes(uint32_t img0, uint32_t cb_col, uint32_t off, uint32_t p) {
+  const uint32_t D = p << 8;  // p rows
+#pragma unroll 1
+  for (uint32_t n0 = 0; n0 < 32; ++n0) {
+    uint32_t a, bit;
+    asm volatile(
+        "v_lshlrev_b32 %0, 3, %2\n\t"
+        "v_and_or_b32 %0, %0, %3, %4\n\t"
+        "v_lshlrev_b32 %1, %2, 1"
+        : "=&v"(a), "=&v"(bit)
+        : "v"(off), "s"(0xffffff00u), "v"(cb_col));
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      mark_at(a, bit);
+      a += D;
+    }
+    const bool in = a < img0 + IMG_BYTES;
+    mark_at((a & (IMG_BYTES - 1)) | img0, in ? bit : 0u);
+    off = opaque(off + p);
+  }
+}
+
 // A: one mid prime (61 < p <= TA) per wave; lane L walks column L =
 // (plane L&7, column L>>3).
 __device__ __forceinline__ void unit_A(uint32_t* __restrict__ img, uint32_t pi, uint64_t m, uint64_t Vs,
@@ -371,6 +425,18 @@ __device__ __forceinline__ void unit_A(uint32_t* __restrict__ img, uint32_t pi, 
   if (p2 <= Vs) {
     const uint32_t cm = mod_small(c * LS, p, invp);
     uint32_t off = kp >= cm ? kp - cm : kp + p - cm;
+    const uint32_t K = ROWS / p;  // wave-uniform, scalar
+    if (p < TA_CLS) {
+      switch (K) {  // ROWS / p for 61 < p < TA_CLS
+        case 2: a_classes<2>(lds_addr(img), cb_col, off, p); return;
+        case 3: a_classes<3>(lds_addr(img), cb_col, off, p); return;
+        case 4: a_classes<4>(lds_addr(img), cb_col, off, p); return;
+        case 5: a_classes<5>(lds_addr(img), cb_col, off, p); return;
+        case 6: a_classes<6>(lds_addr(img), cb_col, off, p); return;
+        case 7: a_classes<7>(lds_addr(img), cb_col, off, p); return;
+        default: break;
+      }
+    }
     const uint32_t n_full = div_small(LS, p, invp);
     off = mark_run(cb_col, off, p, n_full);
     if (off < LS) mark_col(cb_col, off);
