@@ -653,6 +653,10 @@ struct WheelLds {
   unsigned long long wave_cnt[NW];
 };
 
+#ifdef DSE_TIMING
+__device__ unsigned long long g_timing[5];
+#endif
+
 __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restrict__ table, WheelArgs wa,
                                                             uint32_t* __restrict__ out,
                                                             unsigned long long* __restrict__ count_out) {
@@ -673,6 +677,22 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + table_a_offset(th->cap));
 
   const uint32_t tid = threadIdx.x, lane_id = tid & 63, wave = tid >> 6;
+#ifdef DSE_TIMING
+  // profiling builds (tools/build_variant.sh timing -DDSE_TIMING): per-wave
+  // cycles of mark / mark barrier / expand / init / segment barrier, summed
+  // over segments and waves into g_timing (dse_debug_timing)
+  uint64_t t_acc[5] = {0, 0, 0, 0, 0}, t_prev = 0;
+#define DSE_TSTAMP(i)                                              \
+  do {                                                             \
+    const uint64_t t_now = __builtin_amdgcn_s_memtime();           \
+    if ((i) > 0) t_acc[(i) - 1] += t_now - t_prev;                 \
+    t_prev = t_now;                                                \
+  } while (0)
+#else
+#define DSE_TSTAMP(i) \
+  do {                \
+  } while (0)
+#endif
   const bool expander = wave < NE;
 #ifdef DSE_PHASE_KNOB
   const uint32_t phases = wa.phases;  // ablation builds (tools/build_variant.sh knob -DDSE_PHASE_KNOB)
@@ -1025,19 +1045,29 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
 #else
   if (T > 0) init_segment(lds.img[0], blockIdx.x);
   __syncthreads();
+  DSE_TSTAMP(0);
   for (uint32_t t = 0; t < T; ++t) {
     const uint64_t s = blockIdx.x + (uint64_t)t * grid;
     if (phases & kPhaseUnits) mark_segment(lds.img[0], s, 0);
     lds_drain();
+    DSE_TSTAMP(1);
     __syncthreads();
+    DSE_TSTAMP(2);
     if (phases & kPhaseExpand) expand_segment(lds.img[0], s);
+    DSE_TSTAMP(3);
     // init of this workgroup's next segment, on the rows this wave just
     // expanded: no barrier in between, and waves drift into init while
     // others still expand
     if (t + 1 < T) init_segment(lds.img[0], s + grid);
     if (tid == 0) lds.ctr[0] = 0;  // all claims of this segment returned before the barrier above
+    DSE_TSTAMP(4);
     __syncthreads();
+    DSE_TSTAMP(5);
   }
+#endif
+#ifdef DSE_TIMING
+  if (lane_id == 0)
+    for (int i = 0; i < 5; ++i) atomicAdd(&g_timing[i], (unsigned long long)t_acc[i]);
 #endif
 
 #pragma unroll
@@ -1243,6 +1273,15 @@ hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream) {
   hipLaunchKernelGGL(wheel_offsets_kernel, dim3(4 * (uint32_t)num_cus), dim3(256), 0, stream, table);
   return hipGetLastError();
 }
+
+#ifdef DSE_TIMING
+// profiling builds only: read and clear the per-phase cycle sums
+extern "C" int dse_debug_timing(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_timing), sizeof(unsigned long long) * 5) != hipSuccess) return -1;
+  const unsigned long long z[5] = {0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_timing), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 hipError_t free_scratch(Scratch* s) {
   if (!s || !s->ptr) return hipSuccess;
