@@ -654,7 +654,7 @@ struct WheelLds {
 };
 
 #ifdef DSE_TIMING
-__device__ unsigned long long g_timing[5];
+__device__ unsigned long long g_timing[8];
 #endif
 
 __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restrict__ table, WheelArgs wa,
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   // profiling builds (tools/build_variant.sh timing -DDSE_TIMING): per-wave
   // cycles of mark / mark barrier / expand / init / segment barrier, summed
   // over segments and waves into g_timing (dse_debug_timing)
-  uint64_t t_acc[5] = {0, 0, 0, 0, 0}, t_prev = 0;
+  uint64_t t_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_prev = 0;  // + A, B, L unit time (drained)
 #define DSE_TSTAMP(i)                                              \
   do {                                                             \
     const uint64_t t_now = __builtin_amdgcn_s_memtime();           \
@@ -1000,6 +1000,10 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       const uint32_t c2 = claim();  // unit after next, read at the end of this one
       if (u_nxt < n_all && is_l(u_nxt)) load_L(nxt, P, M, A, i_mid1 + 64 * idx_of(u_nxt) + lane, i_big);
       const uint32_t k = idx_of(u_cur);
+#ifdef DSE_TIMING
+      const uint64_t t_u0 = __builtin_amdgcn_s_memtime();
+      const uint32_t u_type = !is_l(u_cur) ? (k < nA ? 5u : 6u) : 7u;
+#endif
       if (!is_l(u_cur)) {
         if (k < nA) {
           const uint32_t pi = __builtin_amdgcn_readfirstlane(s_mid_p[k]);
@@ -1017,6 +1021,10 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p);
         if ((phases & kPhaseLarge) && (uint64_t)p0 * p0 < Vend) unit_L(cur, Vs, Vend, Kb, ps, pl_rot, wa.rho_pack);
       }
+#ifdef DSE_TIMING
+      lds_drain();
+      t_acc[u_type] += __builtin_amdgcn_s_memtime() - t_u0;
+#endif
       cur = nxt;
       u_cur = u_nxt;
       u_nxt = claimed(c2);
@@ -1067,7 +1075,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
 #endif
 #ifdef DSE_TIMING
   if (lane_id == 0)
-    for (int i = 0; i < 5; ++i) atomicAdd(&g_timing[i], (unsigned long long)t_acc[i]);
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_timing[i], (unsigned long long)t_acc[i]);
 #endif
 
 #pragma unroll
@@ -1277,8 +1285,8 @@ hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream) {
 #ifdef DSE_TIMING
 // profiling builds only: read and clear the per-phase cycle sums
 extern "C" int dse_debug_timing(unsigned long long* out) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_timing), sizeof(unsigned long long) * 5) != hipSuccess) return -1;
-  const unsigned long long z[5] = {0, 0, 0, 0, 0};
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_timing), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+  const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_timing), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -10,7 +10,7 @@ _dse.LIB_PATH = os.path.join(ROOT, "variants", os.environ.get("DSE_TIMING_LIB", 
 from mail_sieve_e.sieve import Context
 N = int(float(sys.argv[1])) if len(sys.argv) > 1 else 10**11
 c = Context(1)
-buf = (ctypes.c_ulonglong * 5)()
+buf = (ctypes.c_ulonglong * 8)()
 c.sieve_all(N, 1)                      # warm up
 assert _dse.lib().dse_debug_timing(buf) == 0
 c.sieve_all(N, 1)
@@ -18,7 +18,10 @@ assert _dse.lib().dse_debug_timing(buf) == 0
 waves = 256 * 16
 clk = 2.4e9 / 1e3                      # s_memtime ticks per ms at the 2.4 GHz shader clock (approximate)
 names = ["mark", "mark barrier wait", "expand", "init", "segment barrier wait"]
-tot = sum(buf)
-for n, v in zip(names, buf):
+tot = sum(buf[:5])
+for n, v in zip(names, buf[:5]):
     print(f"{n:22s} {v / waves / clk:7.3f} ms per wave  ({100 * v / tot:5.1f}%)")
 print(f"{'sum':22s} {tot / waves / clk:7.3f} ms per wave")
+for n, v in zip(["  A units", "  B units", "  L units"], buf[5:]):
+    print(f"{n:22s} {v / waves / clk:7.3f} ms per wave  ({100 * v / buf[0]:5.1f}% of mark)")
+print(f"{'  unit loop rest':22s} {(buf[0] - sum(buf[5:])) / waves / clk:7.3f} ms per wave")
