@@ -640,6 +640,28 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
   }
 }
 
+// Bucketed hits of segment s (entries [b0, b1), thread t of T takes every
+// T-th): kBkBatch loads in flight per thread before their marks (one at a
+// time, every entry paid a full global-load latency: the window's wheel
+// kernel spent most of its time here). Not inlined: its registers stay out
+// of the unit loop's allocation.
+__device__ __attribute__((noinline)) void mark_bucket_hits(const uint32_t* __restrict__ ent, uint32_t b0, uint32_t b1,
+                                                         uint32_t t, uint32_t T, uint32_t img0) {
+  constexpr uint32_t kBkBatch = 16;
+  uint32_t j = b0 + t;
+  for (; j + (kBkBatch - 1) * T < b1; j += kBkBatch * T) {
+    uint32_t e[kBkBatch];
+#pragma unroll
+    for (uint32_t q = 0; q < kBkBatch; ++q) e[q] = __builtin_nontemporal_load(ent + j + q * T);
+#pragma unroll
+    for (uint32_t q = 0; q < kBkBatch; ++q) mark_plane<false>(img0 + 4 * (e[q] >> kWheelLogKP), e[q] & (KP - 1));
+  }
+  for (; j < b1; j += T) {
+    const uint32_t e = ent[j];
+    mark_plane<false>(img0 + 4 * (e >> kWheelLogKP), e & (KP - 1));
+  }
+}
+
 struct WheelLds {
   uint32_t img[NIMG][IMG_WORDS];   // the segment image(s), at LDS address 0
   uint64_t mid_m[kMidCap];         // Barrett factors of the staged mid primes
@@ -952,13 +974,8 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     // bucketed hits of the primes > kWheelMaxPrime: one entry per marking
     // thread (pipelined: the non-expander waves)
     constexpr uint32_t kMarkT0 = DSE_PIPELINE ? NE * 64 : 0;
-    if (wa.bk_start && (phases & kPhaseLarge) && tid >= kMarkT0) {
-      const uint32_t b0 = wa.bk_start[s], b1 = wa.bk_start[s + 1];
-      for (uint32_t j = b0 + tid - kMarkT0; j < b1; j += NT - kMarkT0) {
-        const uint32_t e = wa.bk_entries[j];
-        mark_plane<false>(img0 + 4 * (e >> kWheelLogKP), e & (KP - 1));
-      }
-    }
+    if (wa.bk_start && (phases & kPhaseLarge) && tid >= kMarkT0)
+      mark_bucket_hits(wa.bk_entries, wa.bk_start[s], wa.bk_start[s + 1], tid - kMarkT0, NT - kMarkT0, img0);
     const uint32_t rot = (i_mid1 + lane) & 7;  // = table index & 7 of this lane's large primes
     // absolute residue (q + rot) & 7 at step q: its plane and e bit
     const uint32_t pl_rot = ((wa.pl_pack >> (3 * rot)) | (wa.pl_pack << (24 - 3 * rot))) & 0xFFFFFFu;
