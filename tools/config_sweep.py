@@ -13,6 +13,9 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "distributed-sieve-e_amd")]
+from mail_sieve_e import _dse  # noqa: E402
+if os.environ.get("DSE_LIB"):  # A/B another build of the library
+    _dse.LIB_PATH = os.environ["DSE_LIB"]
 from mail_sieve_e import work  # noqa: E402
 from mail_sieve_e.sieve import Context  # noqa: E402
 
