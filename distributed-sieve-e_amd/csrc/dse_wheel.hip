@@ -1159,6 +1159,9 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
 // seeded from the scanned columns). The wheel kernel ORs its segment's list.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kBucketThreads = 256;
+#ifndef DSE_BK_TWO_LEVEL
+#define DSE_BK_TWO_LEVEL 0  // 1: two-level staged fill (A/B builds; measured slower)
+#endif
 #ifndef DSE_BK_GRID
 #define DSE_BK_GRID 1024
 #endif
@@ -1193,9 +1196,9 @@ __global__ void bucket_range_kernel(const void* __restrict__ table, uint64_t vma
   range[1] = lo;
 }
 
-// Walk the coprime-to-30 multiples of p inside [V0 + 1, V0 + span), from p^2 on.
-template <typename Emit>
-__device__ __forceinline__ void bucket_walk(uint32_t p, uint64_t m, const BucketArgs& ba, Emit emit) {
+// First coprime-to-30 multiple of p at or above max(V0 + 1, p^2): its offset
+// o from V0 and 3 * (index of the multiplier mod 30 in R30).
+__device__ __forceinline__ uint64_t bucket_first(uint32_t p, uint64_t m, const BucketArgs& ba, uint32_t& w3) {
   const uint64_t p2 = (uint64_t)p * p;
   const uint64_t vlo = max(ba.V0 + 1, p2);
   uint64_t q = __umul64hi(vlo, m);  // floor(vlo / p), corrected
@@ -1204,14 +1207,28 @@ __device__ __forceinline__ void bucket_walk(uint32_t p, uint64_t m, const Bucket
   const uint64_t m0 = q + (r != 0);
   const uint32_t r30 = (uint32_t)(m0 % 30);
   const uint32_t d = __builtin_ctz(kCoprime30 >> r30);
-  uint32_t w3 = 3 * __popc(kCoprime30 & ((1u << (r30 + d)) - 1));  // 3 * index of (m mod 30) in R30
-  uint64_t o = (uint64_t)p * (m0 + d) - ba.V0;
+  w3 = 3 * __popc(kCoprime30 & ((1u << (r30 + d)) - 1));
+  return (uint64_t)p * (m0 + d) - ba.V0;
+}
+
+// The hit at offset o (< span): its segment and entry k | plane << kWheelLogKP.
+__device__ __forceinline__ uint32_t bucket_entry(uint64_t o, const BucketArgs& ba, uint32_t& s) {
+  s = ((uint32_t)(o >> kWheelLogKP)) / 30u;  // o < 2^34
+  const uint32_t u = (uint32_t)(o - (uint64_t)s * kWheelSpan);
+  const uint32_t k = u / 30u, rho = u - 30u * k;
+  const uint32_t pl = (uint32_t)(ba.plane_lut >> (3 * (rho >> 1))) & 7u;
+  return k | (pl << kWheelLogKP);
+}
+
+// Walk the coprime-to-30 multiples of p inside [V0 + 1, V0 + span), from p^2 on.
+template <typename Emit>
+__device__ __forceinline__ void bucket_walk(uint32_t p, uint64_t m, const BucketArgs& ba, Emit emit) {
+  uint32_t w3;
+  uint64_t o = bucket_first(p, m, ba, w3);
   while (o < ba.span) {
-    const uint32_t s = ((uint32_t)(o >> kWheelLogKP)) / 30u;  // o < 2^34
-    const uint32_t u = (uint32_t)(o - (uint64_t)s * kWheelSpan);
-    const uint32_t k = u / 30u, rho = u - 30u * k;
-    const uint32_t pl = (uint32_t)(ba.plane_lut >> (3 * (rho >> 1))) & 7u;
-    emit(s, k | (pl << kWheelLogKP));
+    uint32_t s;
+    const uint32_t e = bucket_entry(o, ba, s);
+    emit(s, e);
     o += (uint64_t)p * ((kGap30 >> w3) & 7u);
     w3 = w3 == 21 ? 0u : w3 + 3;
   }
@@ -1266,12 +1283,18 @@ __global__ __launch_bounds__(1024) void bucket_startscan_kernel(const uint32_t* 
   }
   uint32_t run = s_scan[tid] - sum;
   for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t t = tot[b];
     start[b] = run;
-    run += tot[b];
+    run += t;
   }
   if (tid == 1023) start[nseg] = s_scan[1023];
 }
 
+#if !DSE_BK_TWO_LEVEL
+// One-level fill: every hit is one dword store at its slot (an LDS cursor per
+// segment). The lanes of a wave walk consecutive primes, so for p below ~1e8
+// a step's hits share a segment and take consecutive slots (one coalesced
+// store); the large primes' hits scatter.
 __global__ __launch_bounds__(kBucketThreads) void bucket_fill_kernel(const void* __restrict__ table, BucketArgs ba,
                                                                    const uint32_t* __restrict__ range,
                                                                    const uint32_t* __restrict__ cols,
@@ -1291,6 +1314,234 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_fill_kernel(const void*
       if (pos < cap) entries[pos] = e;
     });
 }
+#else
+// Two-level fill. A one-level fill stores every hit as its own scattered dword
+// (request-bound, 3.8x write amplification); here every global store is a
+// run of consecutive dwords.
+//
+// Level 1 (bucket_stage_kernel) files each hit under its super-bucket of
+// kSupSegs consecutive segments, key = (segment mod kSupSegs) << 20 | entry.
+// Each wave stages kStageCap keys per super-bucket in LDS and writes a full
+// stage as one run (a whole-wave store) into the workgroup's region of that
+// super-bucket; the region of (workgroup g, super-bucket S) starts at
+//   start[S kSupSegs] + sum over S's segments s of cols[s][g]
+// (cols = per-segment exclusive scans over the workgroups), so the temporary
+// array holds each super-bucket where its segments will end up, workgroups in
+// order. A lane whose stage is full keeps its hit and retries after the flush.
+//
+// Level 2 (bucket_sort_kernel): job (S, group of kSortGroup workgroups) reads
+// its contiguous slice of super-bucket S, whose per-segment counts are known
+// (cols again), and counting-sorts tiles of kSortTile keys by segment in LDS;
+// each segment's run of a tile is stored contiguously at its cursor, which
+// starts at start[s] + cols[s][first workgroup of the group].
+//
+// The lanes of a wave walk consecutive primes, whose hits stay within a few
+// segments of each other: most steps send the whole wave to one stage, and a
+// tile's keys come in runs of a few segments. LDS counters are therefore
+// bumped once per group of equal keys (peers found with one ballot per key
+// bit), never 64 times on one address.
+constexpr uint32_t kSupLog = 7;
+constexpr uint32_t kSupSegs = 1u << kSupLog;       // segments per super-bucket
+constexpr uint32_t kStageCap = 64;                 // keys per (wave, super-bucket) stage: one 256 B run
+constexpr uint32_t kKeyShift = 20;                 // entry = k | plane << 17 < 2^20
+static_assert(kWheelLogKP + 3 <= (int)kKeyShift && kKeyShift + kSupLog <= 32, "bucket key layout");
+constexpr uint32_t kSortGroup = 16;                // level-1 workgroups per level-2 job
+constexpr uint32_t kSortTile = 4096;               // keys per LDS counting sort
+static_assert(kBucketGrid % kSortGroup == 0, "sort groups");
+
+__host__ __device__ constexpr uint32_t stage_lds_words(uint32_t nsup) {
+  return nsup + (kBucketThreads / 64) * nsup * (kStageCap + 1);
+}
+
+// Lanes of the wave whose key (< 2^bits) equals this lane's, among `valid` lanes.
+__device__ __forceinline__ uint64_t key_peers(uint32_t key, bool valid, uint32_t bits) {
+  uint64_t m = __ballot(valid);
+  for (uint32_t b = 0; b < bits; ++b) {
+    const bool set = (key >> b) & 1u;
+    const uint64_t x = __ballot(set);
+    m &= set ? x : ~x;
+  }
+  return m;
+}
+
+// LDS counter += number of peers; returns this lane's slot (old value + rank among its peers).
+__device__ __forceinline__ uint32_t peer_add(uint32_t* ctr, uint64_t peers, bool valid) {
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
+  uint32_t base = 0;
+  if (valid && rank == 0) base = atomicAdd(ctr, (uint32_t)__popcll(peers));
+  const uint32_t leader = valid ? (uint32_t)__builtin_ctzll(peers) : 0u;
+  base = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(leader << 2), (int)base);
+  return base + rank;
+}
+
+__global__ __launch_bounds__(kBucketThreads) void bucket_stage_kernel(const void* __restrict__ table, BucketArgs ba,
+                                                                    const uint32_t* __restrict__ range,
+                                                                    const uint32_t* __restrict__ cols,
+                                                                    const uint32_t* __restrict__ start,
+                                                                    uint32_t* __restrict__ tmp, uint32_t nsup) {
+  extern __shared__ uint32_t sm[];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t* cur = sm;                                          // [nsup] region cursors of this workgroup
+  uint32_t* scnt = sm + nsup + wave * nsup * (kStageCap + 1);  // [nsup] this wave's stage fills
+  uint32_t* stage = scnt + nsup;                               // [nsup][kStageCap]
+  const uint32_t sbits = nsup > 1 ? 32 - __builtin_clz(nsup - 1) : 0;
+  for (uint32_t S = tid; S < nsup; S += kBucketThreads) cur[S] = start[S << kSupLog];
+  for (uint32_t S = lane; S < nsup; S += 64) scnt[S] = 0;
+  __syncthreads();
+  for (uint32_t s = tid; s < ba.nseg; s += kBucketThreads)
+    atomicAdd(&cur[s >> kSupLog], cols[(uint64_t)s * kBucketGrid + blockIdx.x]);
+  __syncthreads();
+
+  const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
+  const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
+  const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
+  const uint32_t i_hi = range[1];
+  constexpr uint32_t stride = kBucketGrid * kBucketThreads;
+  uint32_t i = range[0] + blockIdx.x * kBucketThreads + tid;
+  uint32_t p = 0, w3 = 0;
+  uint64_t o = ba.span;
+  // next prime of this lane with a hit in the pass (o >= span: none left)
+  auto next_prime = [&]() {
+    for (; i < i_hi; i += stride) {
+      p = P[i];
+      o = bucket_first(p, M[i], ba, w3);
+      if (o < ba.span) return;
+    }
+    o = ba.span;
+  };
+  next_prime();
+  while (__ballot(o < ba.span)) {
+    const bool act = o < ba.span;
+    uint32_t S = 0, key = 0;
+    if (act) {
+      uint32_t s;
+      const uint32_t e = bucket_entry(o, ba, s);
+      S = s >> kSupLog;
+      key = ((s & (kSupSegs - 1)) << kKeyShift) | e;
+    }
+    const uint64_t peers = key_peers(S, act, sbits);
+    const uint32_t slot = peer_add(&scnt[S], peers, act);
+    const uint32_t pos = act ? slot : kStageCap;
+    if (pos < kStageCap) stage[S * kStageCap + pos] = key;
+    // stages that just filled: exactly one lane took their last slot and reserves the run
+    const bool filled = pos == kStageCap - 1;
+    uint32_t g = 0;
+    if (filled) g = atomicAdd(&cur[S], kStageCap);
+    uint64_t full = __ballot(filled);
+    __builtin_amdgcn_wave_barrier();
+    while (full) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(full);
+      full &= full - 1;
+      const uint32_t Sf = (uint32_t)__builtin_amdgcn_readlane((int)S, (int)l);
+      const uint32_t gf = (uint32_t)__builtin_amdgcn_readlane((int)g, (int)l);
+      tmp[gf + lane] = stage[Sf * kStageCap + lane];
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) scnt[Sf] = 0;
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (pos < kStageCap) {  // placed: advance to the next hit (or prime)
+      o += (uint64_t)p * ((kGap30 >> w3) & 7u);
+      w3 = w3 == 21 ? 0u : w3 + 3;
+      if (o >= ba.span) {
+        i += stride;
+        next_prime();
+      }
+    }
+  }
+  // partial stages
+  for (uint32_t S = 0; S < nsup; ++S) {
+    const uint32_t n = scnt[S];
+    if (n == 0) continue;
+    uint32_t g = 0;
+    if (lane == 0) g = atomicAdd(&cur[S], n);
+    g = (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
+    if (lane < n) tmp[g + lane] = stage[S * kStageCap + lane];
+  }
+}
+
+__global__ __launch_bounds__(kBucketThreads) void bucket_sort_kernel(BucketArgs ba, const uint32_t* __restrict__ cols,
+                                                                   const uint32_t* __restrict__ start,
+                                                                   const uint32_t* __restrict__ tmp,
+                                                                   uint32_t* __restrict__ entries) {
+  constexpr uint32_t kPer = kSortTile / kBucketThreads;
+  constexpr uint32_t kPerLane = kSupSegs / 64;  // scan: segment counts per lane of wave 0
+  __shared__ uint32_t sorted[kSortTile];
+  __shared__ uint32_t hist[kSupSegs], off[kSupSegs], curs[kSupSegs];
+  __shared__ uint32_t rb[2];
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  constexpr uint32_t ngroups = kBucketGrid / kSortGroup;
+  const uint32_t S = blockIdx.x / ngroups, g0 = (blockIdx.x % ngroups) * kSortGroup, g1 = g0 + kSortGroup;
+  const uint32_t s0 = S << kSupLog;
+  if (tid < 2) rb[tid] = 0;
+  if (tid < kSupSegs) hist[tid] = 0;
+  __syncthreads();
+  if (tid < kSupSegs) {
+    const uint32_t s = s0 + tid;
+    uint32_t c0 = 0, c1 = 0;
+    if (s < ba.nseg) {
+      c0 = cols[(uint64_t)s * kBucketGrid + g0];
+      c1 = g1 < kBucketGrid ? cols[(uint64_t)s * kBucketGrid + g1] : start[s + 1] - start[s];
+      curs[tid] = start[s] + c0;
+    }
+    atomicAdd(&rb[0], c0);
+    atomicAdd(&rb[1], c1);
+  }
+  __syncthreads();
+  const uint32_t r0 = start[s0] + rb[0], r1 = start[s0] + rb[1];
+  for (uint32_t base = r0; base < r1; base += kSortTile) {
+    const uint32_t n = min(kSortTile, r1 - base);
+    uint32_t key[kPer], rk[kPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q) {
+      const uint32_t j = q * kBucketThreads + tid;
+      key[q] = j < n ? __builtin_nontemporal_load(tmp + base + j) : 0u;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q) {
+      const bool v = q * kBucketThreads + tid < n;
+      const uint32_t k = key[q] >> kKeyShift;
+      rk[q] = peer_add(&hist[k], key_peers(k, v, kSupLog), v);
+    }
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the segment counts (one wave, kPerLane each)
+      uint32_t c[kPerLane], sum = 0;
+#pragma unroll
+      for (uint32_t t = 0; t < kPerLane; ++t) sum += (c[t] = hist[lane * kPerLane + t]);
+      uint32_t x = sum;
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+      }
+      x -= sum;
+#pragma unroll
+      for (uint32_t t = 0; t < kPerLane; ++t) {
+        off[lane * kPerLane + t] = x;
+        x += c[t];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q)
+      if (q * kBucketThreads + tid < n) sorted[off[key[q] >> kKeyShift] + rk[q]] = key[q];
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q) {
+      const uint32_t j = q * kBucketThreads + tid;
+      if (j < n) {
+        const uint32_t v = sorted[j], k = v >> kKeyShift;
+        entries[curs[k] + j - off[k]] = v & ((1u << kKeyShift) - 1);
+      }
+    }
+    __syncthreads();
+    if (tid < kSupSegs) {
+      curs[tid] += hist[tid];
+      hist[tid] = 0;
+    }
+    __syncthreads();
+  }
+}
+#endif
 
 }  // namespace
 
@@ -1443,9 +1694,10 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     ba.nseg = (uint32_t)ns;
     ba.vmax = vmax_p;
     const uint64_t cap = bucket_cap(ba.span, (double)kWheelMaxPrime, (double)isqrt64(vmax_p));
-    // scratch: [range 2][cols grid*ns][tot ns][start ns+1][entries cap]
+    // scratch: [range 2][cols grid*ns][tot ns][start ns+1][entries cap][level-1 keys cap]
     const uint64_t o_cols = 256, o_tot = o_cols + 4ull * kBucketGrid * ns, o_start = o_tot + 4 * ns + 256,
-                   o_ent = (o_start + 4 * (ns + 1) + 255) & ~255ull, bytes = o_ent + 4 * cap;
+                   o_ent = (o_start + 4 * (ns + 1) + 255) & ~255ull, o_tmp = (o_ent + 4 * cap + 255) & ~255ull,
+                   bytes = DSE_BK_TWO_LEVEL ? o_tmp + 4 * cap : o_ent + 4 * cap;
     char* sc = nullptr;
     hipError_t e = ensure_scratch(scratch, bytes, stream, &sc);
     if (e != hipSuccess) return e;
@@ -1454,13 +1706,28 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     uint32_t* tot = reinterpret_cast<uint32_t*>(sc + o_tot);
     uint32_t* start = reinterpret_cast<uint32_t*>(sc + o_start);
     uint32_t* ent = reinterpret_cast<uint32_t*>(sc + o_ent);
+    uint32_t* tmp = reinterpret_cast<uint32_t*>(sc + o_tmp);
+    (void)tmp;
     hipLaunchKernelGGL(bucket_range_kernel, dim3(1), dim3(1), 0, stream, table, vmax_p, range);
     hipLaunchKernelGGL(bucket_count_kernel, dim3(kBucketGrid), dim3(kBucketThreads), 0, stream, table, ba, range, cols);
     hipLaunchKernelGGL(bucket_colscan_kernel, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, stream, cols,
                        (uint32_t)ns, tot);
     hipLaunchKernelGGL(bucket_startscan_kernel, dim3(1), dim3(1024), 0, stream, tot, (uint32_t)ns, start);
+#if DSE_BK_TWO_LEVEL
+    const uint32_t nsup = (uint32_t)((ns + kSupSegs - 1) >> kSupLog);
+    const uint32_t stage_bytes = 4 * stage_lds_words(nsup);
+    if (stage_bytes > 65536 &&
+        (e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bucket_stage_kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)stage_bytes)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(bucket_stage_kernel, dim3(kBucketGrid), dim3(kBucketThreads), stage_bytes, stream,
+                       table, ba, range, cols, start, tmp, nsup);
+    hipLaunchKernelGGL(bucket_sort_kernel, dim3(nsup * (kBucketGrid / kSortGroup)), dim3(kBucketThreads), 0, stream,
+                       ba, cols, start, tmp, ent);
+#else
     hipLaunchKernelGGL(bucket_fill_kernel, dim3(kBucketGrid), dim3(kBucketThreads), 0, stream, table, ba, range, cols,
                        start, ent, cap);
+#endif
     if ((e = hipGetLastError()) != hipSuccess) return e;
     wa.bk_entries = ent;
     wa.bk_start = start;
