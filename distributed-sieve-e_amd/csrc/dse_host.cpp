@@ -522,6 +522,11 @@ int32_t dse_debug_set_option(dse_ctx* ctx, const char* name, int64_t value) {
     ctx->opts.bucket_pass_segs = (uint32_t)value;
     return DSE_OK;
   }
+  if (n == "bucket_split_log2") {
+    if (value < 0 || value > 63) return fail(DSE_EINVAL, "bucket_split_log2 out of range");
+    ctx->opts.bucket_split_log2 = (uint32_t)value;
+    return DSE_OK;
+  }
   return fail(DSE_EINVAL, "unknown option " + n);
 }
 

@@ -66,6 +66,7 @@ hipError_t free_scratch(Scratch* s);
 // defaults are the production configuration. No environment variable is read.
 struct SieveOpts {
   uint32_t bucket_pass_segs = 0;  // > 0: cap the segments per bucket pass (multi-pass coverage)
+  uint32_t bucket_split_log2 = 0; // > 0: bucketed primes <= 2^k filled one level, above two levels (0: production)
 };
 
 hipError_t launch_base_primes(uint64_t limit, void* table, uint32_t cap, hipStream_t stream);

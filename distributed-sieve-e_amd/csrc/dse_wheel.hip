@@ -1159,16 +1159,25 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
 // seeded from the scanned columns). The wheel kernel ORs its segment's list.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kBucketThreads = 256;
-#ifndef DSE_BK_TWO_LEVEL
-#define DSE_BK_TWO_LEVEL 0  // 1: two-level staged fill (A/B builds; measured slower)
-#endif
 #ifndef DSE_BK_GRID
 #define DSE_BK_GRID 1024
 #endif
 #ifndef DSE_BK_SEGS
 #define DSE_BK_SEGS 8192
 #endif
-constexpr uint32_t kBucketGrid = DSE_BK_GRID;    // workgroups of the count / fill walks
+#ifndef DSE_BK_GRID1
+#define DSE_BK_GRID1 4096
+#endif
+// Two bands of bucketed primes: band 0 (p <= split, kBucketGrid workgroups)
+// is filled one level, band 1 (p > split, kBucketGrid1 workgroups) staged in
+// two levels. The count kernel's columns are the kBucketGrid + kBucketGrid1
+// "virtual workgroups", band 0 first, so within a segment band 0's entries
+// precede band 1's.
+constexpr uint32_t kBucketGrid = DSE_BK_GRID;
+constexpr uint32_t kBucketGrid1 = DSE_BK_GRID1;
+constexpr uint32_t kBucketCols = kBucketGrid + kBucketGrid1;
+static_assert(kBucketCols % 64 == 0, "column scan: whole lanes");
+constexpr uint32_t kBucketSplitLog = 26;           // production split: primes <= 2^26 one-level
 constexpr uint32_t kBucketMaxSegs = DSE_BK_SEGS; // segments per pass (LDS counters)
 constexpr uint32_t kCoprime30 = (1u << 1) | (1u << 7) | (1u << 11) | (1u << 13) | (1u << 17) | (1u << 19) |
                                 (1u << 23) | (1u << 29);
@@ -1181,19 +1190,28 @@ struct BucketArgs {
   uint64_t plane_lut;  // plane of relative residue rho (odd) in bits [3(rho >> 1), +3)
   uint32_t nseg;       // segments in the pass (<= kBucketMaxSegs)
   uint64_t vmax;       // largest value of the pass (primes with p^2 > vmax have no hits)
+  uint64_t split;      // band 0: kWheelMaxPrime < p <= split, band 1: p > split
 };
 
-// i_lo = first table index with p > kWheelMaxPrime, i_hi = first with p^2 > vmax
-__global__ void bucket_range_kernel(const void* __restrict__ table, uint64_t vmax, uint32_t* __restrict__ range) {
+// range[0] = first table index with p > kWheelMaxPrime, range[1] = first with
+// p^2 > vmax, range[2] = first with p > split (clamped to [range[0], range[1]])
+__global__ void bucket_range_kernel(const void* __restrict__ table, uint64_t vmax, uint64_t split,
+                                    uint32_t* __restrict__ range) {
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
   const uint32_t np = th->count == 0xFFFFFFFFu ? 0u : th->count;
   const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
   uint32_t lo = 0, hi = np;
   while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= kWheelMaxPrime) lo = mid + 1; else hi = mid; }
   range[0] = lo;
+  const uint32_t i_lo = lo;
   hi = np;
   while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if ((uint64_t)P[mid] * P[mid] <= vmax) lo = mid + 1; else hi = mid; }
   range[1] = lo;
+  const uint32_t i_hi = lo;
+  lo = i_lo;
+  hi = i_hi;
+  while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= split) lo = mid + 1; else hi = mid; }
+  range[2] = lo;
 }
 
 // First coprime-to-30 multiple of p at or above max(V0 + 1, p^2): its offset
@@ -1223,15 +1241,15 @@ __device__ __forceinline__ uint32_t bucket_entry(uint64_t o, const BucketArgs& b
 #ifndef DSE_BK_PREFETCH
 #define DSE_BK_PREFETCH 1
 #endif
-// Grid-strided walk over this thread's bucketed primes [i_lo, i_hi): each
+// Grid-strided walk (workgroup b of its band) over this thread's bucketed primes [i_lo, i_hi): each
 // prime's (p, m) is loaded one prime ahead, so the load's latency hides behind
 // the previous prime's walk (loaded on demand, a thread's ~200 primes were a
 // chain of dependent global loads: ~0.7 ms per walk at the 1e18 window).
 template <typename Walk>
 __device__ __forceinline__ void for_bucket_primes(const uint32_t* __restrict__ P, const uint64_t* __restrict__ M,
-                                                  uint32_t i_lo, uint32_t i_hi, Walk walk) {
-  constexpr uint32_t stride = kBucketGrid * kBucketThreads;
-  uint32_t i = i_lo + blockIdx.x * kBucketThreads + threadIdx.x;
+                                                  uint32_t i_lo, uint32_t i_hi, uint32_t b, uint32_t stride,
+                                                  Walk walk) {
+  uint32_t i = i_lo + b * kBucketThreads + threadIdx.x;
 #if DSE_BK_PREFETCH
   if (i >= i_hi) return;
   uint32_t pn = P[i];
@@ -1273,26 +1291,41 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(const void
   const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
   for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) cnt[j] = 0;
   __syncthreads();
-  const uint32_t i_lo = range[0], i_hi = range[1];
-  for_bucket_primes(P, M, i_lo, i_hi, [&](uint32_t p, uint64_t m) {
+  // workgroup x: column x, band 0 below kBucketGrid
+  const uint32_t band = blockIdx.x >= kBucketGrid;
+  const uint32_t i_lo = band ? range[2] : range[0], i_hi = band ? range[1] : range[2];
+  for_bucket_primes(P, M, i_lo, i_hi, blockIdx.x - band * kBucketGrid,
+                    (band ? kBucketGrid1 : kBucketGrid) * kBucketThreads, [&](uint32_t p, uint64_t m) {
     bucket_walk(p, m, ba, [&](uint32_t sg, uint32_t) { atomicAdd(&cnt[sg], 1u); });
   });
   __syncthreads();
-  for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) cols[(uint64_t)j * kBucketGrid + blockIdx.x] = cnt[j];
+  for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) cols[(uint64_t)j * kBucketCols + blockIdx.x] = cnt[j];
 }
 
-// per segment: exclusive scan of its column over the workgroups, in place; total -> tot[s]
-__global__ void bucket_colscan_kernel(uint32_t* __restrict__ cols, uint32_t nseg, uint32_t* __restrict__ tot) {
-  const uint32_t sg = blockIdx.x * blockDim.x + threadIdx.x;
+// per segment (one wave each): exclusive scan of its row over the virtual
+// workgroups, in place; total -> tot[s]
+__global__ __launch_bounds__(256) void bucket_colscan_kernel(uint32_t* __restrict__ cols, uint32_t nseg,
+                                                             uint32_t* __restrict__ tot) {
+  constexpr uint32_t kPer = kBucketCols / 64;
+  const uint32_t sg = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (sg >= nseg) return;
-  uint32_t* c = cols + (uint64_t)sg * kBucketGrid;
-  uint32_t run = 0;
-  for (uint32_t g = 0; g < kBucketGrid; ++g) {
-    const uint32_t v = c[g];
-    c[g] = run;
-    run += v;
+  uint32_t* c = cols + (uint64_t)sg * kBucketCols + lane * kPer;
+  uint32_t v[kPer], sum = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < kPer; ++t) sum += (v[t] = c[t]);
+  uint32_t x = sum;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
   }
-  tot[sg] = run;
+  if (lane == 63) tot[sg] = x;
+  x -= sum;
+#pragma unroll
+  for (uint32_t t = 0; t < kPer; ++t) {
+    c[t] = x;
+    x += v[t];
+  }
 }
 
 // exclusive scan of the segment totals -> start[0..nseg]
@@ -1321,11 +1354,11 @@ __global__ __launch_bounds__(1024) void bucket_startscan_kernel(const uint32_t* 
   if (tid == 1023) start[nseg] = s_scan[1023];
 }
 
-#if !DSE_BK_TWO_LEVEL
-// One-level fill: every hit is one dword store at its slot (an LDS cursor per
-// segment). The lanes of a wave walk consecutive primes, so for p below ~1e8
-// a step's hits share a segment and take consecutive slots (one coalesced
-// store); the large primes' hits scatter.
+// Band 0, one-level fill: every hit is one dword store at its slot (an LDS
+// cursor per segment). The lanes of a wave walk consecutive primes, so for
+// small p a step's hits share a segment and take consecutive slots (one
+// coalesced store); the larger the primes, the more a step's stores scatter
+// (2.7 ps per hit below 2^24, 12 ps above 2^28 at the 1e18 window), hence band 1.
 __global__ __launch_bounds__(kBucketThreads) void bucket_fill_kernel(const void* __restrict__ table, BucketArgs ba,
                                                                    const uint32_t* __restrict__ range,
                                                                    const uint32_t* __restrict__ cols,
@@ -1335,56 +1368,151 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_fill_kernel(const void*
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
   const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
   const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
+  const uint32_t i_lo = range[0], i_hi = range[2];
+  if (i_lo >= i_hi) return;
   for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads)
-    cur[j] = start[j] + cols[(uint64_t)j * kBucketGrid + blockIdx.x];
+    cur[j] = start[j] + cols[(uint64_t)j * kBucketCols + blockIdx.x];
   __syncthreads();
-  const uint32_t i_lo = range[0], i_hi = range[1];
-  for_bucket_primes(P, M, i_lo, i_hi, [&](uint32_t p, uint64_t m) {
+  for_bucket_primes(P, M, i_lo, i_hi, blockIdx.x, kBucketGrid * kBucketThreads, [&](uint32_t p, uint64_t m) {
     bucket_walk(p, m, ba, [&](uint32_t sg, uint32_t e) {
       const uint32_t pos = atomicAdd(&cur[sg], 1u);
       if (pos < cap) entries[pos] = e;
     });
   });
 }
-#else
-// Two-level fill. A one-level fill stores every hit as its own scattered dword
-// (request-bound, 3.8x write amplification); here every global store is a
-// run of consecutive dwords.
+
+// Band 1, two-level fill: every global store is a run of consecutive dwords.
 //
 // Level 1 (bucket_stage_kernel) files each hit under its super-bucket of
 // kSupSegs consecutive segments, key = (segment mod kSupSegs) << 20 | entry.
-// Each wave stages kStageCap keys per super-bucket in LDS and writes a full
-// stage as one run (a whole-wave store) into the workgroup's region of that
-// super-bucket; the region of (workgroup g, super-bucket S) starts at
-//   start[S kSupSegs] + sum over S's segments s of cols[s][g]
-// (cols = per-segment exclusive scans over the workgroups), so the temporary
-// array holds each super-bucket where its segments will end up, workgroups in
-// order. A lane whose stage is full keeps its hit and retries after the flush.
+// Each wave stages kStageCap keys per super-bucket in LDS (a slot per lane
+// from an LDS atomic) and writes a full stage as one 256 B run into its
+// workgroup's region of that super-bucket; the region of (band-1 workgroup g,
+// super-bucket S) starts at
+//   start[S kSupSegs] + sum over S's segments s of cols[s][kBucketGrid + g]
+// (cols = per-segment exclusive scans over the virtual workgroups), so the
+// temporary array holds each super-bucket where its band-1 entries will end
+// up. A lane whose stage is full keeps its hit and retries after the flush.
+// Lanes move on to their next prime independently, its (p, m) loaded one
+// prime ahead (a wave-synchronous walk that waited on that load at every
+// prime change was latency-bound).
 //
-// Level 2 (bucket_sort_kernel): job (S, group of kSortGroup workgroups) reads
-// its contiguous slice of super-bucket S, whose per-segment counts are known
-// (cols again), and counting-sorts tiles of kSortTile keys by segment in LDS;
+// Level 2 (bucket_sort_kernel): job (S, group of kSortGroup band-1
+// workgroups) reads its contiguous slice of super-bucket S, whose per-segment
+// counts are known (cols again), and counting-sorts tiles of kSortTile keys by
+// segment in LDS, the next tile's keys loaded while the current one sorts;
 // each segment's run of a tile is stored contiguously at its cursor, which
 // starts at start[s] + cols[s][first workgroup of the group].
-//
-// The lanes of a wave walk consecutive primes, whose hits stay within a few
-// segments of each other: most steps send the whole wave to one stage, and a
-// tile's keys come in runs of a few segments. LDS counters are therefore
-// bumped once per group of equal keys (peers found with one ballot per key
-// bit), never 64 times on one address.
 constexpr uint32_t kSupLog = 7;
 constexpr uint32_t kSupSegs = 1u << kSupLog;       // segments per super-bucket
 constexpr uint32_t kStageCap = 64;                 // keys per (wave, super-bucket) stage: one 256 B run
 constexpr uint32_t kKeyShift = 20;                 // entry = k | plane << 17 < 2^20
 static_assert(kWheelLogKP + 3 <= (int)kKeyShift && kKeyShift + kSupLog <= 32, "bucket key layout");
-constexpr uint32_t kSortGroup = 16;                // level-1 workgroups per level-2 job
+#ifndef DSE_BK_SORT_GROUP
+#define DSE_BK_SORT_GROUP 4
+#endif
+#ifndef DSE_BK_SORT_PEERS
+#define DSE_BK_SORT_PEERS 0  // 1: tile histogram bumped once per group of equal keys (ballots), A/B
+#endif
+constexpr uint32_t kSortGroup = DSE_BK_SORT_GROUP;  // band-1 workgroups per level-2 job
 constexpr uint32_t kSortTile = 4096;               // keys per LDS counting sort
-static_assert(kBucketGrid % kSortGroup == 0, "sort groups");
+static_assert(kBucketGrid1 % kSortGroup == 0, "sort groups");
 
 __host__ __device__ constexpr uint32_t stage_lds_words(uint32_t nsup) {
   return nsup + (kBucketThreads / 64) * nsup * (kStageCap + 1);
 }
 
+__global__ __launch_bounds__(kBucketThreads) void bucket_stage_kernel(const void* __restrict__ table, BucketArgs ba,
+                                                                    const uint32_t* __restrict__ range,
+                                                                    const uint32_t* __restrict__ cols,
+                                                                    const uint32_t* __restrict__ start,
+                                                                    uint32_t* __restrict__ tmp, uint32_t nsup) {
+  extern __shared__ uint32_t sm[];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t i_hi = range[1];
+  constexpr uint32_t stride = kBucketGrid1 * kBucketThreads;
+  uint32_t i = range[2] + blockIdx.x * kBucketThreads + tid;  // index of the prefetched prime
+  if (__syncthreads_or(i < i_hi) == 0) return;
+  uint32_t* cur = sm;                                          // [nsup] region cursors of this workgroup
+  uint32_t* scnt = sm + nsup + wave * nsup * (kStageCap + 1);  // [nsup] this wave's stage fills
+  uint32_t* stage = scnt + nsup;                               // [nsup][kStageCap]
+  for (uint32_t S = tid; S < nsup; S += kBucketThreads) cur[S] = start[S << kSupLog];
+  for (uint32_t S = lane; S < nsup; S += 64) scnt[S] = 0;
+  __syncthreads();
+  for (uint32_t s = tid; s < ba.nseg; s += kBucketThreads)
+    atomicAdd(&cur[s >> kSupLog], cols[(uint64_t)s * kBucketCols + kBucketGrid + blockIdx.x]);
+  __syncthreads();
+
+  const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
+  const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
+  const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
+  uint32_t pn = 0;
+  uint64_t mn = 0;
+  if (i < i_hi) {
+    pn = P[i];
+    mn = M[i];
+  }
+  uint32_t p = 0, w3 = 0;
+  uint64_t o = ba.span;
+  // next prime of this lane with a hit in the pass (o >= span: none left)
+  auto next_prime = [&]() {
+    while (i < i_hi) {
+      p = pn;
+      const uint64_t m = mn;
+      i += stride;
+      if (i < i_hi) {
+        pn = P[i];
+        mn = M[i];
+      }
+      o = bucket_first(p, m, ba, w3);
+      if (o < ba.span) return;
+    }
+    o = ba.span;
+  };
+  next_prime();
+  while (__ballot(o < ba.span)) {
+    uint32_t S = 0, pos = kStageCap;
+    if (o < ba.span) {
+      uint32_t s;
+      const uint32_t e = bucket_entry(o, ba, s);
+      S = s >> kSupLog;
+      pos = atomicAdd(&scnt[S], 1u);
+      if (pos < kStageCap) stage[S * kStageCap + pos] = ((s & (kSupSegs - 1)) << kKeyShift) | e;
+    }
+    // stages that just filled: exactly one lane took their last slot and reserves the run
+    const bool filled = pos == kStageCap - 1;
+    uint32_t g = 0;
+    if (filled) g = atomicAdd(&cur[S], kStageCap);
+    uint64_t full = __ballot(filled);
+    __builtin_amdgcn_wave_barrier();
+    while (full) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(full);
+      full &= full - 1;
+      const uint32_t Sf = (uint32_t)__builtin_amdgcn_readlane((int)S, (int)l);
+      const uint32_t gf = (uint32_t)__builtin_amdgcn_readlane((int)g, (int)l);
+      tmp[gf + lane] = stage[Sf * kStageCap + lane];
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) scnt[Sf] = 0;  // lanes that overshot the full stage retry next step
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (pos < kStageCap) {  // placed: advance to the next hit (or prime)
+      o += (uint64_t)p * ((kGap30 >> w3) & 7u);
+      w3 = w3 == 21 ? 0u : w3 + 3;
+      if (o >= ba.span) next_prime();
+    }
+  }
+  // partial stages
+  for (uint32_t S = 0; S < nsup; ++S) {
+    const uint32_t n = scnt[S];
+    if (n == 0) continue;
+    uint32_t g = 0;
+    if (lane == 0) g = atomicAdd(&cur[S], n);
+    g = (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
+    if (lane < n) tmp[g + lane] = stage[S * kStageCap + lane];
+  }
+}
+
+#if DSE_BK_SORT_PEERS
 // Lanes of the wave whose key (< 2^bits) equals this lane's, among `valid` lanes.
 __device__ __forceinline__ uint64_t key_peers(uint32_t key, bool valid, uint32_t bits) {
   uint64_t m = __ballot(valid);
@@ -1405,91 +1533,7 @@ __device__ __forceinline__ uint32_t peer_add(uint32_t* ctr, uint64_t peers, bool
   base = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(leader << 2), (int)base);
   return base + rank;
 }
-
-__global__ __launch_bounds__(kBucketThreads) void bucket_stage_kernel(const void* __restrict__ table, BucketArgs ba,
-                                                                    const uint32_t* __restrict__ range,
-                                                                    const uint32_t* __restrict__ cols,
-                                                                    const uint32_t* __restrict__ start,
-                                                                    uint32_t* __restrict__ tmp, uint32_t nsup) {
-  extern __shared__ uint32_t sm[];
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  uint32_t* cur = sm;                                          // [nsup] region cursors of this workgroup
-  uint32_t* scnt = sm + nsup + wave * nsup * (kStageCap + 1);  // [nsup] this wave's stage fills
-  uint32_t* stage = scnt + nsup;                               // [nsup][kStageCap]
-  const uint32_t sbits = nsup > 1 ? 32 - __builtin_clz(nsup - 1) : 0;
-  for (uint32_t S = tid; S < nsup; S += kBucketThreads) cur[S] = start[S << kSupLog];
-  for (uint32_t S = lane; S < nsup; S += 64) scnt[S] = 0;
-  __syncthreads();
-  for (uint32_t s = tid; s < ba.nseg; s += kBucketThreads)
-    atomicAdd(&cur[s >> kSupLog], cols[(uint64_t)s * kBucketGrid + blockIdx.x]);
-  __syncthreads();
-
-  const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
-  const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
-  const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
-  const uint32_t i_hi = range[1];
-  constexpr uint32_t stride = kBucketGrid * kBucketThreads;
-  uint32_t i = range[0] + blockIdx.x * kBucketThreads + tid;
-  uint32_t p = 0, w3 = 0;
-  uint64_t o = ba.span;
-  // next prime of this lane with a hit in the pass (o >= span: none left)
-  auto next_prime = [&]() {
-    for (; i < i_hi; i += stride) {
-      p = P[i];
-      o = bucket_first(p, M[i], ba, w3);
-      if (o < ba.span) return;
-    }
-    o = ba.span;
-  };
-  next_prime();
-  while (__ballot(o < ba.span)) {
-    const bool act = o < ba.span;
-    uint32_t S = 0, key = 0;
-    if (act) {
-      uint32_t s;
-      const uint32_t e = bucket_entry(o, ba, s);
-      S = s >> kSupLog;
-      key = ((s & (kSupSegs - 1)) << kKeyShift) | e;
-    }
-    const uint64_t peers = key_peers(S, act, sbits);
-    const uint32_t slot = peer_add(&scnt[S], peers, act);
-    const uint32_t pos = act ? slot : kStageCap;
-    if (pos < kStageCap) stage[S * kStageCap + pos] = key;
-    // stages that just filled: exactly one lane took their last slot and reserves the run
-    const bool filled = pos == kStageCap - 1;
-    uint32_t g = 0;
-    if (filled) g = atomicAdd(&cur[S], kStageCap);
-    uint64_t full = __ballot(filled);
-    __builtin_amdgcn_wave_barrier();
-    while (full) {
-      const uint32_t l = (uint32_t)__builtin_ctzll(full);
-      full &= full - 1;
-      const uint32_t Sf = (uint32_t)__builtin_amdgcn_readlane((int)S, (int)l);
-      const uint32_t gf = (uint32_t)__builtin_amdgcn_readlane((int)g, (int)l);
-      tmp[gf + lane] = stage[Sf * kStageCap + lane];
-      __builtin_amdgcn_wave_barrier();
-      if (lane == 0) scnt[Sf] = 0;
-      __builtin_amdgcn_wave_barrier();
-    }
-    if (pos < kStageCap) {  // placed: advance to the next hit (or prime)
-      o += (uint64_t)p * ((kGap30 >> w3) & 7u);
-      w3 = w3 == 21 ? 0u : w3 + 3;
-      if (o >= ba.span) {
-        i += stride;
-        next_prime();
-      }
-    }
-  }
-  // partial stages
-  for (uint32_t S = 0; S < nsup; ++S) {
-    const uint32_t n = scnt[S];
-    if (n == 0) continue;
-    uint32_t g = 0;
-    if (lane == 0) g = atomicAdd(&cur[S], n);
-    g = (uint32_t)__builtin_amdgcn_readfirstlane((int)g);
-    if (lane < n) tmp[g + lane] = stage[S * kStageCap + lane];
-  }
-}
+#endif
 
 __global__ __launch_bounds__(kBucketThreads) void bucket_sort_kernel(BucketArgs ba, const uint32_t* __restrict__ cols,
                                                                    const uint32_t* __restrict__ start,
@@ -1501,8 +1545,9 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_sort_kernel(BucketArgs 
   __shared__ uint32_t hist[kSupSegs], off[kSupSegs], curs[kSupSegs];
   __shared__ uint32_t rb[2];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
-  constexpr uint32_t ngroups = kBucketGrid / kSortGroup;
-  const uint32_t S = blockIdx.x / ngroups, g0 = (blockIdx.x % ngroups) * kSortGroup, g1 = g0 + kSortGroup;
+  constexpr uint32_t ngroups = kBucketGrid1 / kSortGroup;
+  const uint32_t S = blockIdx.x / ngroups, g0 = kBucketGrid + (blockIdx.x % ngroups) * kSortGroup,
+                 g1 = g0 + kSortGroup;
   const uint32_t s0 = S << kSupLog;
   if (tid < 2) rb[tid] = 0;
   if (tid < kSupSegs) hist[tid] = 0;
@@ -1511,8 +1556,8 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_sort_kernel(BucketArgs 
     const uint32_t s = s0 + tid;
     uint32_t c0 = 0, c1 = 0;
     if (s < ba.nseg) {
-      c0 = cols[(uint64_t)s * kBucketGrid + g0];
-      c1 = g1 < kBucketGrid ? cols[(uint64_t)s * kBucketGrid + g1] : start[s + 1] - start[s];
+      c0 = cols[(uint64_t)s * kBucketCols + g0];
+      c1 = g1 < kBucketCols ? cols[(uint64_t)s * kBucketCols + g1] : start[s + 1] - start[s];
       curs[tid] = start[s] + c0;
     }
     atomicAdd(&rb[0], c0);
@@ -1520,20 +1565,33 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_sort_kernel(BucketArgs 
   }
   __syncthreads();
   const uint32_t r0 = start[s0] + rb[0], r1 = start[s0] + rb[1];
+  uint32_t nxt[kPer];
+  auto load_tile = [&](uint32_t base) {
+    const uint32_t n = min(kSortTile, r1 - base);
+#pragma unroll
+    for (uint32_t q = 0; q < kPer; ++q) {
+      const uint32_t j = q * kBucketThreads + tid;
+      nxt[q] = j < n ? __builtin_nontemporal_load(tmp + base + j) : 0u;
+    }
+  };
+  if (r0 < r1) load_tile(r0);
   for (uint32_t base = r0; base < r1; base += kSortTile) {
     const uint32_t n = min(kSortTile, r1 - base);
     uint32_t key[kPer], rk[kPer];
 #pragma unroll
-    for (uint32_t q = 0; q < kPer; ++q) {
-      const uint32_t j = q * kBucketThreads + tid;
-      key[q] = j < n ? __builtin_nontemporal_load(tmp + base + j) : 0u;
-    }
+    for (uint32_t q = 0; q < kPer; ++q) key[q] = nxt[q];
+    if (base + kSortTile < r1) load_tile(base + kSortTile);
 #pragma unroll
-    for (uint32_t q = 0; q < kPer; ++q) {
+    for (uint32_t q = 0; q < kPer; ++q)
+#if DSE_BK_SORT_PEERS
+    {
       const bool v = q * kBucketThreads + tid < n;
       const uint32_t k = key[q] >> kKeyShift;
       rk[q] = peer_add(&hist[k], key_peers(k, v, kSupLog), v);
     }
+#else
+      rk[q] = q * kBucketThreads + tid < n ? atomicAdd(&hist[key[q] >> kKeyShift], 1u) : 0u;
+#endif
     __syncthreads();
     if (tid < 64) {  // exclusive scan of the segment counts (one wave, kPerLane each)
       uint32_t c[kPerLane], sum = 0;
@@ -1573,7 +1631,6 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_sort_kernel(BucketArgs 
     __syncthreads();
   }
 }
-#endif
 
 }  // namespace
 
@@ -1725,11 +1782,14 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     ba.plane_lut = plane_lut;
     ba.nseg = (uint32_t)ns;
     ba.vmax = vmax_p;
-    const uint64_t cap = bucket_cap(ba.span, (double)kWheelMaxPrime, (double)isqrt64(vmax_p));
-    // scratch: [range 2][cols grid*ns][tot ns][start ns+1][entries cap][level-1 keys cap]
-    const uint64_t o_cols = 256, o_tot = o_cols + 4ull * kBucketGrid * ns, o_start = o_tot + 4 * ns + 256,
+    const uint64_t root_p = isqrt64(vmax_p);
+    const uint64_t cap = bucket_cap(ba.span, (double)kWheelMaxPrime, (double)root_p);
+    ba.split = 1ull << (opts && opts->bucket_split_log2 ? opts->bucket_split_log2 : kBucketSplitLog);
+    const bool band0 = ba.split > kWheelMaxPrime, band1 = ba.split < root_p;
+    // scratch: [range 3][cols 2*grid*ns][tot ns][start ns+1][entries cap][band-1 level-1 keys cap]
+    const uint64_t o_cols = 256, o_tot = o_cols + 4ull * kBucketCols * ns, o_start = o_tot + 4 * ns + 256,
                    o_ent = (o_start + 4 * (ns + 1) + 255) & ~255ull, o_tmp = (o_ent + 4 * cap + 255) & ~255ull,
-                   bytes = DSE_BK_TWO_LEVEL ? o_tmp + 4 * cap : o_ent + 4 * cap;
+                   bytes = band1 ? o_tmp + 4 * cap : o_ent + 4 * cap;
     char* sc = nullptr;
     hipError_t e = ensure_scratch(scratch, bytes, stream, &sc);
     if (e != hipSuccess) return e;
@@ -1739,27 +1799,26 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     uint32_t* start = reinterpret_cast<uint32_t*>(sc + o_start);
     uint32_t* ent = reinterpret_cast<uint32_t*>(sc + o_ent);
     uint32_t* tmp = reinterpret_cast<uint32_t*>(sc + o_tmp);
-    (void)tmp;
-    hipLaunchKernelGGL(bucket_range_kernel, dim3(1), dim3(1), 0, stream, table, vmax_p, range);
-    hipLaunchKernelGGL(bucket_count_kernel, dim3(kBucketGrid), dim3(kBucketThreads), 0, stream, table, ba, range, cols);
-    hipLaunchKernelGGL(bucket_colscan_kernel, dim3((uint32_t)((ns + 255) / 256)), dim3(256), 0, stream, cols,
+    hipLaunchKernelGGL(bucket_range_kernel, dim3(1), dim3(1), 0, stream, table, vmax_p, ba.split, range);
+    hipLaunchKernelGGL(bucket_count_kernel, dim3(kBucketCols), dim3(kBucketThreads), 0, stream, table, ba, range, cols);
+    hipLaunchKernelGGL(bucket_colscan_kernel, dim3((uint32_t)((ns + 3) / 4)), dim3(256), 0, stream, cols,
                        (uint32_t)ns, tot);
     hipLaunchKernelGGL(bucket_startscan_kernel, dim3(1), dim3(1024), 0, stream, tot, (uint32_t)ns, start);
-#if DSE_BK_TWO_LEVEL
-    const uint32_t nsup = (uint32_t)((ns + kSupSegs - 1) >> kSupLog);
-    const uint32_t stage_bytes = 4 * stage_lds_words(nsup);
-    if (stage_bytes > 65536 &&
-        (e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bucket_stage_kernel),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)stage_bytes)) != hipSuccess)
-      return e;
-    hipLaunchKernelGGL(bucket_stage_kernel, dim3(kBucketGrid), dim3(kBucketThreads), stage_bytes, stream,
-                       table, ba, range, cols, start, tmp, nsup);
-    hipLaunchKernelGGL(bucket_sort_kernel, dim3(nsup * (kBucketGrid / kSortGroup)), dim3(kBucketThreads), 0, stream,
-                       ba, cols, start, tmp, ent);
-#else
-    hipLaunchKernelGGL(bucket_fill_kernel, dim3(kBucketGrid), dim3(kBucketThreads), 0, stream, table, ba, range, cols,
-                       start, ent, cap);
-#endif
+    if (band0)
+      hipLaunchKernelGGL(bucket_fill_kernel, dim3(kBucketGrid), dim3(kBucketThreads), 0, stream, table, ba, range,
+                         cols, start, ent, cap);
+    if (band1) {
+      const uint32_t nsup = (uint32_t)((ns + kSupSegs - 1) >> kSupLog);
+      const uint32_t stage_bytes = 4 * stage_lds_words(nsup);
+      if (stage_bytes > 65536 &&
+          (e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bucket_stage_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)stage_bytes)) != hipSuccess)
+        return e;
+      hipLaunchKernelGGL(bucket_stage_kernel, dim3(kBucketGrid1), dim3(kBucketThreads), stage_bytes, stream, table, ba,
+                         range, cols, start, tmp, nsup);
+      hipLaunchKernelGGL(bucket_sort_kernel, dim3(nsup * (kBucketGrid1 / kSortGroup)), dim3(kBucketThreads), 0,
+                         stream, ba, cols, start, tmp, ent);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     wa.bk_entries = ent;
     wa.bk_start = start;

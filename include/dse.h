@@ -170,6 +170,8 @@ int32_t dse_sieve_range_dev_async(dse_ctx *ctx, const void *table_dev, uint64_t 
  * environment variable; defaults are the production configuration):
  *   "bucket_pass_segments" = k > 0: bucketed passes of at most k segments
  *   (covers the multi-pass path on small windows); 0 = default.
+ *   "bucket_split_log2" = k in 1..63: bucketed primes <= 2^k take the
+ *   one-level fill, larger ones the two-level staged fill; 0 = default.
  * DSE_EINVAL for an unknown name or a value out of range. */
 int32_t dse_debug_set_option(dse_ctx *ctx, const char *name, int64_t value);
 

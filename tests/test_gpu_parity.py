@@ -376,6 +376,25 @@ def test_bucket_multi_pass_mask(oracle):
     assert c == c_ref and np.array_equal(m, m_ref)
 
 
+@pytest.mark.parametrize("split", [21, 23, 25, 63])
+def test_bucket_bands_mask(oracle, split):
+    """Band split of the bucketed primes (test-only option bucket_split_log2):
+    p <= 2^split one-level fill, above it the staged two-level fill. At 1e16
+    the bucketed primes run from 2^21 to 1e8 = 2^26.6: all two-level (21),
+    two splits inside, all one-level (63); in one pass and in passes of 3
+    segments, bit-exact. The production split is covered by every window test."""
+    from mail_sieve_e import sieve as S
+    g0, nb = 10**16 // 2 + 12345, 20 * 983040 + 777
+    m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
+    with S.Context(num_gpus=1) as c:
+        c.debug_set_option("bucket_split_log2", split)
+        m, cnt = c.sieve_odd_range(g0, nb)
+        assert cnt == c_ref and np.array_equal(m, m_ref)
+        c.debug_set_option("bucket_pass_segments", 3)
+        m, cnt = c.sieve_odd_range(g0, nb)
+        assert cnt == c_ref and np.array_equal(m, m_ref)
+
+
 def test_bucket_scratch_freed_with_context():
     """Each context owns its bucketed-pass scratch and dse_destroy frees it:
     creating and destroying contexts that sieve a 1e18 slice must not shrink
