@@ -1359,21 +1359,20 @@ __global__ __launch_bounds__(1024) void bucket_startscan_kernel(const uint32_t* 
 // small p a step's hits share a segment and take consecutive slots (one
 // coalesced store); the larger the primes, the more a step's stores scatter
 // (2.7 ps per hit below 2^24, 12 ps above 2^28 at the 1e18 window), hence band 1.
-__global__ __launch_bounds__(kBucketThreads) void bucket_fill_kernel(const void* __restrict__ table, BucketArgs ba,
-                                                                   const uint32_t* __restrict__ range,
-                                                                   const uint32_t* __restrict__ cols,
-                                                                   const uint32_t* __restrict__ start,
-                                                                   uint32_t* __restrict__ entries, uint64_t cap) {
-  __shared__ uint32_t cur[kBucketMaxSegs];
+// (band-0 workgroup b; cur: nseg words of LDS)
+__device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const void* __restrict__ table,
+                                               const BucketArgs& ba, const uint32_t* __restrict__ range,
+                                               const uint32_t* __restrict__ cols, const uint32_t* __restrict__ start,
+                                               uint32_t* __restrict__ entries, uint64_t cap) {
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
   const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
   const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
   const uint32_t i_lo = range[0], i_hi = range[2];
   if (i_lo >= i_hi) return;
   for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads)
-    cur[j] = start[j] + cols[(uint64_t)j * kBucketCols + blockIdx.x];
+    cur[j] = start[j] + cols[(uint64_t)j * kBucketCols + b];
   __syncthreads();
-  for_bucket_primes(P, M, i_lo, i_hi, blockIdx.x, kBucketGrid * kBucketThreads, [&](uint32_t p, uint64_t m) {
+  for_bucket_primes(P, M, i_lo, i_hi, b, kBucketGrid * kBucketThreads, [&](uint32_t p, uint64_t m) {
     bucket_walk(p, m, ba, [&](uint32_t sg, uint32_t e) {
       const uint32_t pos = atomicAdd(&cur[sg], 1u);
       if (pos < cap) entries[pos] = e;
@@ -1415,23 +1414,30 @@ static_assert(kWheelLogKP + 3 <= (int)kKeyShift && kKeyShift + kSupLog <= 32, "b
 #define DSE_BK_SORT_PEERS 0  // 1: tile histogram bumped once per group of equal keys (ballots), A/B
 #endif
 constexpr uint32_t kSortGroup = DSE_BK_SORT_GROUP;  // band-1 workgroups per level-2 job
-constexpr uint32_t kSortTile = 4096;               // keys per LDS counting sort
+#ifndef DSE_BK_SORT_TILE
+#define DSE_BK_SORT_TILE 4096
+#endif
+constexpr uint32_t kSortTile = DSE_BK_SORT_TILE;   // keys per LDS counting sort
+#ifndef DSE_BK_SORT_THREADS
+#define DSE_BK_SORT_THREADS 1024
+#endif
+constexpr uint32_t kSortThreads = DSE_BK_SORT_THREADS;
+static_assert(kSortTile % kSortThreads == 0 && kSortThreads >= kSupSegs, "sort tile");
 static_assert(kBucketGrid1 % kSortGroup == 0, "sort groups");
 
 __host__ __device__ constexpr uint32_t stage_lds_words(uint32_t nsup) {
   return nsup + (kBucketThreads / 64) * nsup * (kStageCap + 1);
 }
 
-__global__ __launch_bounds__(kBucketThreads) void bucket_stage_kernel(const void* __restrict__ table, BucketArgs ba,
-                                                                    const uint32_t* __restrict__ range,
-                                                                    const uint32_t* __restrict__ cols,
-                                                                    const uint32_t* __restrict__ start,
-                                                                    uint32_t* __restrict__ tmp, uint32_t nsup) {
-  extern __shared__ uint32_t sm[];
+// (band-1 workgroup b; sm: stage_lds_words(nsup) words of LDS)
+__device__ __forceinline__ void bucket_stage_wg(uint32_t* sm, uint32_t b, const void* __restrict__ table,
+                                                const BucketArgs& ba, const uint32_t* __restrict__ range,
+                                                const uint32_t* __restrict__ cols, const uint32_t* __restrict__ start,
+                                                uint32_t* __restrict__ tmp, uint32_t nsup) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t i_hi = range[1];
   constexpr uint32_t stride = kBucketGrid1 * kBucketThreads;
-  uint32_t i = range[2] + blockIdx.x * kBucketThreads + tid;  // index of the prefetched prime
+  uint32_t i = range[2] + b * kBucketThreads + tid;  // index of the prefetched prime
   if (__syncthreads_or(i < i_hi) == 0) return;
   uint32_t* cur = sm;                                          // [nsup] region cursors of this workgroup
   uint32_t* scnt = sm + nsup + wave * nsup * (kStageCap + 1);  // [nsup] this wave's stage fills
@@ -1440,7 +1446,7 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_stage_kernel(const void
   for (uint32_t S = lane; S < nsup; S += 64) scnt[S] = 0;
   __syncthreads();
   for (uint32_t s = tid; s < ba.nseg; s += kBucketThreads)
-    atomicAdd(&cur[s >> kSupLog], cols[(uint64_t)s * kBucketCols + kBucketGrid + blockIdx.x]);
+    atomicAdd(&cur[s >> kSupLog], cols[(uint64_t)s * kBucketCols + kBucketGrid + b]);
   __syncthreads();
 
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
@@ -1512,6 +1518,29 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_stage_kernel(const void
   }
 }
 
+#ifndef DSE_BK_STAGE_FIRST
+#define DSE_BK_STAGE_FIRST 0  // 1: dispatch the band-1 stage workgroups first (A/B)
+#endif
+// Band-0 fill and band-1 stage in one launch: workgroups [0, nfill) fill,
+// the rest stage, so the request-bound scattered stores of the one and the
+// latency-bound staging of the other share the CUs (and neither pays a tail).
+__global__ __launch_bounds__(kBucketThreads) void bucket_fill_stage_kernel(
+    const void* __restrict__ table, BucketArgs ba, const uint32_t* __restrict__ range,
+    const uint32_t* __restrict__ cols, const uint32_t* __restrict__ start, uint32_t* __restrict__ entries,
+    uint64_t cap, uint32_t* __restrict__ tmp, uint32_t nsup, uint32_t nfill) {
+  extern __shared__ uint32_t sm[];
+#if DSE_BK_STAGE_FIRST
+  const uint32_t n1 = gridDim.x - nfill;
+  const uint32_t x = blockIdx.x < n1 ? nfill + blockIdx.x : blockIdx.x - n1;
+#else
+  const uint32_t x = blockIdx.x;
+#endif
+  if (x < nfill)
+    bucket_fill_wg(sm, x, table, ba, range, cols, start, entries, cap);
+  else
+    bucket_stage_wg(sm, x - nfill, table, ba, range, cols, start, tmp, nsup);
+}
+
 #if DSE_BK_SORT_PEERS
 // Lanes of the wave whose key (< 2^bits) equals this lane's, among `valid` lanes.
 __device__ __forceinline__ uint64_t key_peers(uint32_t key, bool valid, uint32_t bits) {
@@ -1535,11 +1564,11 @@ __device__ __forceinline__ uint32_t peer_add(uint32_t* ctr, uint64_t peers, bool
 }
 #endif
 
-__global__ __launch_bounds__(kBucketThreads) void bucket_sort_kernel(BucketArgs ba, const uint32_t* __restrict__ cols,
+__global__ __launch_bounds__(kSortThreads) void bucket_sort_kernel(BucketArgs ba, const uint32_t* __restrict__ cols,
                                                                    const uint32_t* __restrict__ start,
                                                                    const uint32_t* __restrict__ tmp,
                                                                    uint32_t* __restrict__ entries) {
-  constexpr uint32_t kPer = kSortTile / kBucketThreads;
+  constexpr uint32_t kPer = kSortTile / kSortThreads;
   constexpr uint32_t kPerLane = kSupSegs / 64;  // scan: segment counts per lane of wave 0
   __shared__ uint32_t sorted[kSortTile];
   __shared__ uint32_t hist[kSupSegs], off[kSupSegs], curs[kSupSegs];
@@ -1570,7 +1599,7 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_sort_kernel(BucketArgs 
     const uint32_t n = min(kSortTile, r1 - base);
 #pragma unroll
     for (uint32_t q = 0; q < kPer; ++q) {
-      const uint32_t j = q * kBucketThreads + tid;
+      const uint32_t j = q * kSortThreads + tid;
       nxt[q] = j < n ? __builtin_nontemporal_load(tmp + base + j) : 0u;
     }
   };
@@ -1585,12 +1614,12 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_sort_kernel(BucketArgs 
     for (uint32_t q = 0; q < kPer; ++q)
 #if DSE_BK_SORT_PEERS
     {
-      const bool v = q * kBucketThreads + tid < n;
+      const bool v = q * kSortThreads + tid < n;
       const uint32_t k = key[q] >> kKeyShift;
       rk[q] = peer_add(&hist[k], key_peers(k, v, kSupLog), v);
     }
 #else
-      rk[q] = q * kBucketThreads + tid < n ? atomicAdd(&hist[key[q] >> kKeyShift], 1u) : 0u;
+      rk[q] = q * kSortThreads + tid < n ? atomicAdd(&hist[key[q] >> kKeyShift], 1u) : 0u;
 #endif
     __syncthreads();
     if (tid < 64) {  // exclusive scan of the segment counts (one wave, kPerLane each)
@@ -1613,11 +1642,11 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_sort_kernel(BucketArgs 
     __syncthreads();
 #pragma unroll
     for (uint32_t q = 0; q < kPer; ++q)
-      if (q * kBucketThreads + tid < n) sorted[off[key[q] >> kKeyShift] + rk[q]] = key[q];
+      if (q * kSortThreads + tid < n) sorted[off[key[q] >> kKeyShift] + rk[q]] = key[q];
     __syncthreads();
 #pragma unroll
     for (uint32_t q = 0; q < kPer; ++q) {
-      const uint32_t j = q * kBucketThreads + tid;
+      const uint32_t j = q * kSortThreads + tid;
       if (j < n) {
         const uint32_t v = sorted[j], k = v >> kKeyShift;
         entries[curs[k] + j - off[k]] = v & ((1u << kKeyShift) - 1);
@@ -1804,19 +1833,17 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     hipLaunchKernelGGL(bucket_colscan_kernel, dim3((uint32_t)((ns + 3) / 4)), dim3(256), 0, stream, cols,
                        (uint32_t)ns, tot);
     hipLaunchKernelGGL(bucket_startscan_kernel, dim3(1), dim3(1024), 0, stream, tot, (uint32_t)ns, start);
-    if (band0)
-      hipLaunchKernelGGL(bucket_fill_kernel, dim3(kBucketGrid), dim3(kBucketThreads), 0, stream, table, ba, range,
-                         cols, start, ent, cap);
+    const uint32_t nsup = (uint32_t)((ns + kSupSegs - 1) >> kSupLog);
+    const uint32_t nfill = band0 ? kBucketGrid : 0;
+    const uint32_t lds_bytes = std::max(band0 ? 4 * (uint32_t)ns : 0u, band1 ? 4 * stage_lds_words(nsup) : 0u);
+    if (lds_bytes > 65536 &&
+        (e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bucket_fill_stage_kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(bucket_fill_stage_kernel, dim3(nfill + (band1 ? kBucketGrid1 : 0)), dim3(kBucketThreads),
+                       lds_bytes, stream, table, ba, range, cols, start, ent, cap, tmp, nsup, nfill);
     if (band1) {
-      const uint32_t nsup = (uint32_t)((ns + kSupSegs - 1) >> kSupLog);
-      const uint32_t stage_bytes = 4 * stage_lds_words(nsup);
-      if (stage_bytes > 65536 &&
-          (e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bucket_stage_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)stage_bytes)) != hipSuccess)
-        return e;
-      hipLaunchKernelGGL(bucket_stage_kernel, dim3(kBucketGrid1), dim3(kBucketThreads), stage_bytes, stream, table, ba,
-                         range, cols, start, tmp, nsup);
-      hipLaunchKernelGGL(bucket_sort_kernel, dim3(nsup * (kBucketGrid1 / kSortGroup)), dim3(kBucketThreads), 0,
+      hipLaunchKernelGGL(bucket_sort_kernel, dim3(nsup * (kBucketGrid1 / kSortGroup)), dim3(kSortThreads), 0,
                          stream, ba, cols, start, tmp, ent);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
