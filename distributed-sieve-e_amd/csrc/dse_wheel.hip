@@ -1408,14 +1408,14 @@ constexpr uint32_t kStageCap = 64;                 // keys per (wave, super-buck
 constexpr uint32_t kKeyShift = 20;                 // entry = k | plane << 17 < 2^20
 static_assert(kWheelLogKP + 3 <= (int)kKeyShift && kKeyShift + kSupLog <= 32, "bucket key layout");
 #ifndef DSE_BK_SORT_GROUP
-#define DSE_BK_SORT_GROUP 4
+#define DSE_BK_SORT_GROUP 16
 #endif
 #ifndef DSE_BK_SORT_PEERS
 #define DSE_BK_SORT_PEERS 0  // 1: tile histogram bumped once per group of equal keys (ballots), A/B
 #endif
 constexpr uint32_t kSortGroup = DSE_BK_SORT_GROUP;  // band-1 workgroups per level-2 job
 #ifndef DSE_BK_SORT_TILE
-#define DSE_BK_SORT_TILE 4096
+#define DSE_BK_SORT_TILE 8192
 #endif
 constexpr uint32_t kSortTile = DSE_BK_SORT_TILE;   // keys per LDS counting sort
 #ifndef DSE_BK_SORT_THREADS
