@@ -30,6 +30,7 @@ namespace {
 constexpr uint32_t kCompactWordsPerThread = 2;
 constexpr uint32_t kCompactThreads = 256;
 constexpr uint32_t kCompactBlockWords = kCompactWordsPerThread * kCompactThreads;  // 512 words
+constexpr uint32_t kCompactStage = 8192;  // LDS slots for a block's primes (32 KiB)
 
 __global__ __launch_bounds__(kCompactThreads) void compact_count_kernel(const uint64_t* __restrict__ mask,
                                                                         uint64_t words,
@@ -88,6 +89,7 @@ __global__ __launch_bounds__(kCompactThreads) void compact_write_kernel(const ui
                                                                         const uint32_t* __restrict__ block_offs,
                                                                         uint32_t* __restrict__ P, uint32_t cap) {
   __shared__ uint32_t s_scan[kCompactThreads];
+  __shared__ uint32_t s_stage[kCompactStage];
   const uint32_t tid = threadIdx.x;
   const uint64_t w0 = (uint64_t)blockIdx.x * kCompactBlockWords + tid * kCompactWordsPerThread;
   uint64_t v[kCompactWordsPerThread];
@@ -105,17 +107,31 @@ __global__ __launch_bounds__(kCompactThreads) void compact_write_kernel(const ui
     s_scan[tid] += x;
     __syncthreads();
   }
-  uint32_t pos = block_offs[blockIdx.x] + s_scan[tid] - c;
+  // the block's primes are staged in LDS in order, then stored as one
+  // contiguous run (each thread's primes are consecutive slots, so direct
+  // stores would put a wave's lanes ~a dozen slots apart: one line each);
+  // slots past kCompactStage (never at the densest block, 6,542 primes) go
+  // straight to global memory
+  const uint32_t base = block_offs[blockIdx.x], total = s_scan[kCompactThreads - 1];
+  uint32_t pos = s_scan[tid] - c;
 #pragma unroll
   for (uint32_t k = 0; k < kCompactWordsPerThread; ++k) {
     uint64_t x = v[k];
     while (x) {
       const uint32_t b = __ffsll((long long)x) - 1;
       x &= x - 1;
-      if (pos < cap) P[pos] = (uint32_t)(3 + 2 * ((w0 + k) * 64 + b));
+      const uint32_t q = (uint32_t)(3 + 2 * ((w0 + k) * 64 + b));
+      if (pos < kCompactStage)
+        s_stage[pos] = q;
+      else if (base + pos < cap)
+        P[base + pos] = q;
       ++pos;
     }
   }
+  __syncthreads();
+  const uint32_t n = min(total, kCompactStage);
+  for (uint32_t j = tid; j < n; j += kCompactThreads)
+    if (base + j < cap) P[base + j] = s_stage[j];
 }
 
 // ---------------------------------------------------------------------------
@@ -229,7 +245,7 @@ hipError_t launch_base_primes_big(uint64_t limit, void* table, uint32_t cap, int
   hipLaunchKernelGGL(compact_write_kernel, dim3(nblocks), dim3(kCompactThreads), 0, stream, mask, words, sums, P,
                      cap);
   if ((e = hipGetLastError()) != hipSuccess) return e;
-  return launch_wheel_offsets(table, num_cus, stream);  // m[] and a[]
+  return launch_wheel_offsets(table, num_cus, stream, cap);  // m[] and a[]
 }
 
 }  // namespace dse

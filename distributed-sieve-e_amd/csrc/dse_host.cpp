@@ -168,7 +168,7 @@ int32_t share_table(dse_ctx* ctx, uint64_t limit) {
   for (int i = 1; i < nd; ++i) {
     DevState& d = ctx->devs[i];
     HIP_TRY(hipSetDevice(d.device));
-    HIP_TRY(dse::launch_wheel_offsets(d.table, d.num_cus, d.stream));
+    HIP_TRY(dse::launch_wheel_offsets(d.table, d.num_cus, d.stream, prime_cap(limit)));
   }
   return DSE_OK;
 }
@@ -316,7 +316,7 @@ int32_t dse_base_table_finish_dev_async(dse_ctx* ctx, uint64_t limit, void* tabl
   if (table_bytes < dse_base_table_bytes(limit)) return fail(DSE_EINVAL, "table buffer too small");
   if (limit > dse::kBigBaseLimitMax) return fail(DSE_ERANGE, "base-prime limit above the supported maximum");
   HIP_TRY(hipSetDevice(ctx->devs[0].device));
-  HIP_TRY(dse::launch_wheel_offsets(table_dev, ctx->devs[0].num_cus, (hipStream_t)stream));
+  HIP_TRY(dse::launch_wheel_offsets(table_dev, ctx->devs[0].num_cus, (hipStream_t)stream, prime_cap(limit)));
   return DSE_OK;
 }
 

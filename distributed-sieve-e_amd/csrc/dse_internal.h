@@ -83,6 +83,7 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
                               unsigned long long* count, int num_cus, hipStream_t stream, Scratch* scratch,
                               const SieveOpts* opts);
 // Fill the Barrett factors m[] and wheel offsets a[] of a table whose p[] is final.
-hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream);
+// n_hint: table capacity when known (sizes the grid: about 4 primes per thread)
+hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream, uint64_t n_hint = 0);
 
 }  // namespace dse

@@ -1663,8 +1663,9 @@ __global__ __launch_bounds__(kSortThreads) void bucket_sort_kernel(BucketArgs ba
 
 }  // namespace
 
-hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream) {
-  hipLaunchKernelGGL(wheel_offsets_kernel, dim3(4 * (uint32_t)num_cus), dim3(256), 0, stream, table);
+hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream, uint64_t n_hint) {
+  const uint64_t grid = std::max<uint64_t>(4 * (uint64_t)num_cus, std::min<uint64_t>(n_hint / 1024 + 1, 1u << 16));
+  hipLaunchKernelGGL(wheel_offsets_kernel, dim3((uint32_t)grid), dim3(256), 0, stream, table);
   return hipGetLastError();
 }
 
