@@ -43,7 +43,10 @@ constexpr int kWheelLogKP = DSE_WHEEL_LOG_KP;
 constexpr uint64_t kWheelSpan = 30ull << kWheelLogKP;   // integers per segment
 constexpr uint64_t kWheelOutBits = kWheelSpan / 2;      // odd candidates per segment
 // Base primes above this go through the bucketed pass (dse_wheel.hip).
-constexpr uint64_t kWheelMaxPrime = 1ull << 21;
+#ifndef DSE_WHEEL_MAX_LOG
+#define DSE_WHEEL_MAX_LOG 20  // A/B builds only (window: 2^21 7.95 ms, 2^20 7.85, 2^19 8.30)
+#endif
+constexpr uint64_t kWheelMaxPrime = 1ull << DSE_WHEEL_MAX_LOG;
 
 // Largest limit the single-workgroup base-prime kernel handles (LDS bitmap).
 constexpr uint64_t kBaseLimitMax = 2ull * 150u * 1024u * 8u + 1ull;  // 150 KiB of odd bits

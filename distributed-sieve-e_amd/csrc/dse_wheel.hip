@@ -1177,7 +1177,7 @@ constexpr uint32_t kBucketGrid = DSE_BK_GRID;
 constexpr uint32_t kBucketGrid1 = DSE_BK_GRID1;
 constexpr uint32_t kBucketCols = kBucketGrid + kBucketGrid1;
 static_assert(kBucketCols % 64 == 0, "column scan: whole lanes");
-constexpr uint32_t kBucketSplitLog = 26;           // production split: primes <= 2^26 one-level
+constexpr uint32_t kBucketSplitLog = 25;           // production split: primes <= 2^25 one-level
 constexpr uint32_t kBucketMaxSegs = DSE_BK_SEGS; // segments per pass (LDS counters)
 constexpr uint32_t kCoprime30 = (1u << 1) | (1u << 7) | (1u << 11) | (1u << 13) | (1u << 17) | (1u << 19) |
                                 (1u << 23) | (1u << 29);

@@ -328,7 +328,7 @@ def test_table_from_broadcast_primes(ctx, limit):
     n = int(full[:4].cpu().view(torch.int32)[0])
     assert torch.equal(full[m_off:m_off + 8 * n], part[m_off:m_off + 8 * n])  # Barrett factors
     P = full[16:16 + 4 * n].cpu().view(torch.int32).numpy()
-    n_rows = int(np.searchsorted(P, 1 << 21, side="right"))                 # rows exist for p <= 2^21
+    n_rows = int(np.searchsorted(P, 1 << 20, side="right"))                 # rows exist for p <= 2^20
     assert torch.equal(full[a_off:a_off + 32 * n_rows], part[a_off:a_off + 32 * n_rows])
     g0, nb = (limit * limit) // 2 - 5_000_000, 4_000_000
     outs = []
@@ -353,10 +353,10 @@ def test_kb_float_quotient_boundary(ctx, oracle):
     assert c == c_ref and np.array_equal(m, m_ref)
 
 
-# ---- bucketed pass (primes > 2^21) ----
+# ---- bucketed pass (primes > 2^20) ----
 
 def test_bucket_threshold_window_vs_oracle(ctx, oracle):
-    """1e13: base primes up to 3.16e6, the ones above 2^21 go through buckets."""
+    """1e13: base primes up to 3.16e6, the ones above 2^20 go through buckets."""
     g0, nb = (10**13 + 1 - 3) // 2, 5 * 10**7
     m, c = ctx.sieve_odd_range(g0, nb)
     m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
@@ -376,11 +376,11 @@ def test_bucket_multi_pass_mask(oracle):
     assert c == c_ref and np.array_equal(m, m_ref)
 
 
-@pytest.mark.parametrize("split", [21, 23, 25, 63])
+@pytest.mark.parametrize("split", [20, 23, 25, 63])
 def test_bucket_bands_mask(oracle, split):
     """Band split of the bucketed primes (test-only option bucket_split_log2):
     p <= 2^split one-level fill, above it the staged two-level fill. At 1e16
-    the bucketed primes run from 2^21 to 1e8 = 2^26.6: all two-level (21),
+    the bucketed primes run from 2^20 to 1e8 = 2^26.6: all two-level (20),
     two splits inside, all one-level (63); in one pass and in passes of 3
     segments, bit-exact. The production split is covered by every window test."""
     from mail_sieve_e import sieve as S
