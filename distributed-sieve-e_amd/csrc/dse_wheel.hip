@@ -1238,34 +1238,41 @@ __device__ __forceinline__ uint32_t bucket_entry(uint64_t o, const BucketArgs& b
   return k | (pl << kWheelLogKP);
 }
 
-#ifndef DSE_BK_PREFETCH
-#define DSE_BK_PREFETCH 1
+#ifndef DSE_BK_SNAKE
+#define DSE_BK_SNAKE 1  // 0: band 0 in plain grid-stride order (A/B)
 #endif
-// Grid-strided walk (workgroup b of its band) over this thread's bucketed primes [i_lo, i_hi): each
-// prime's (p, m) is loaded one prime ahead, so the load's latency hides behind
-// the previous prime's walk (loaded on demand, a thread's ~200 primes were a
-// chain of dependent global loads: ~0.7 ms per walk at the 1e18 window).
+// Grid-strided walk (workgroup b of its band) over this thread's bucketed
+// primes [i_lo, i_hi): each prime's (p, m) is loaded one prime ahead, so the
+// load's latency hides behind the previous prime's walk (loaded on demand, a
+// thread's ~200 primes were a chain of dependent global loads: ~0.7 ms per
+// walk at the 1e18 window). snake: odd rounds of the stride take their block
+// in reverse thread order, so the thread with one round's smallest prime (the
+// most hits, ~1/p) gets the next round's largest; in plain order the threads
+// holding a band's smallest primes walk up to ~1.7x the mean.
 template <typename Walk>
 __device__ __forceinline__ void for_bucket_primes(const uint32_t* __restrict__ P, const uint64_t* __restrict__ M,
                                                   uint32_t i_lo, uint32_t i_hi, uint32_t b, uint32_t stride,
-                                                  Walk walk) {
-  uint32_t i = i_lo + b * kBucketThreads + threadIdx.x;
-#if DSE_BK_PREFETCH
+                                                  bool snake, Walk walk) {
+  const uint32_t j = b * kBucketThreads + threadIdx.x;
+  const uint32_t jr = DSE_BK_SNAKE && snake ? stride - 1 - j : j;
+  uint32_t base = i_lo, i = i_lo + j;
   if (i >= i_hi) return;
   uint32_t pn = P[i];
   uint64_t mn = M[i];
-  for (; i < i_hi; i += stride) {
+  for (bool odd = false;;) {  // round indices increase, so the first one past i_hi ends the walk
     const uint32_t p = pn;
     const uint64_t m = mn;
-    if (i + stride < i_hi) {
-      pn = P[i + stride];
-      mn = M[i + stride];
+    base += stride;
+    odd = !odd;
+    i = base + (odd ? jr : j);
+    const bool more = i < i_hi;
+    if (more) {
+      pn = P[i];
+      mn = M[i];
     }
     walk(p, m);
+    if (!more) break;
   }
-#else
-  for (; i < i_hi; i += stride) walk(P[i], M[i]);
-#endif
 }
 
 // Walk the coprime-to-30 multiples of p inside [V0 + 1, V0 + span), from p^2 on.
@@ -1285,7 +1292,7 @@ __device__ __forceinline__ void bucket_walk(uint32_t p, uint64_t m, const Bucket
 __global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(const void* __restrict__ table, BucketArgs ba,
                                                                     const uint32_t* __restrict__ range,
                                                                     uint32_t* __restrict__ cols) {
-  __shared__ uint32_t cnt[kBucketMaxSegs];
+  extern __shared__ uint32_t cnt[];  // [nseg]
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
   const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
   const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
@@ -1295,7 +1302,7 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(const void
   const uint32_t band = blockIdx.x >= kBucketGrid;
   const uint32_t i_lo = band ? range[2] : range[0], i_hi = band ? range[1] : range[2];
   for_bucket_primes(P, M, i_lo, i_hi, blockIdx.x - band * kBucketGrid,
-                    (band ? kBucketGrid1 : kBucketGrid) * kBucketThreads, [&](uint32_t p, uint64_t m) {
+                    (band ? kBucketGrid1 : kBucketGrid) * kBucketThreads, band == 0, [&](uint32_t p, uint64_t m) {
     bucket_walk(p, m, ba, [&](uint32_t sg, uint32_t) { atomicAdd(&cnt[sg], 1u); });
   });
   __syncthreads();
@@ -1372,7 +1379,7 @@ __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const 
   for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads)
     cur[j] = start[j] + cols[(uint64_t)j * kBucketCols + b];
   __syncthreads();
-  for_bucket_primes(P, M, i_lo, i_hi, b, kBucketGrid * kBucketThreads, [&](uint32_t p, uint64_t m) {
+  for_bucket_primes(P, M, i_lo, i_hi, b, kBucketGrid * kBucketThreads, true, [&](uint32_t p, uint64_t m) {
     bucket_walk(p, m, ba, [&](uint32_t sg, uint32_t e) {
       const uint32_t pos = atomicAdd(&cur[sg], 1u);
       if (pos < cap) entries[pos] = e;
@@ -1830,7 +1837,8 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     uint32_t* ent = reinterpret_cast<uint32_t*>(sc + o_ent);
     uint32_t* tmp = reinterpret_cast<uint32_t*>(sc + o_tmp);
     hipLaunchKernelGGL(bucket_range_kernel, dim3(1), dim3(1), 0, stream, table, vmax_p, ba.split, range);
-    hipLaunchKernelGGL(bucket_count_kernel, dim3(kBucketCols), dim3(kBucketThreads), 0, stream, table, ba, range, cols);
+    hipLaunchKernelGGL(bucket_count_kernel, dim3(kBucketCols), dim3(kBucketThreads), 4 * (uint32_t)ns, stream, table,
+                       ba, range, cols);
     hipLaunchKernelGGL(bucket_colscan_kernel, dim3((uint32_t)((ns + 3) / 4)), dim3(256), 0, stream, cols,
                        (uint32_t)ns, tot);
     hipLaunchKernelGGL(bucket_startscan_kernel, dim3(1), dim3(1024), 0, stream, tot, (uint32_t)ns, start);
