@@ -1417,9 +1417,6 @@ static_assert(kWheelLogKP + 3 <= (int)kKeyShift && kKeyShift + kSupLog <= 32, "b
 #ifndef DSE_BK_SORT_GROUP
 #define DSE_BK_SORT_GROUP 16
 #endif
-#ifndef DSE_BK_SORT_PEERS
-#define DSE_BK_SORT_PEERS 0  // 1: tile histogram bumped once per group of equal keys (ballots), A/B
-#endif
 constexpr uint32_t kSortGroup = DSE_BK_SORT_GROUP;  // band-1 workgroups per level-2 job
 #ifndef DSE_BK_SORT_TILE
 #define DSE_BK_SORT_TILE 8192
@@ -1525,9 +1522,6 @@ __device__ __forceinline__ void bucket_stage_wg(uint32_t* sm, uint32_t b, const 
   }
 }
 
-#ifndef DSE_BK_STAGE_FIRST
-#define DSE_BK_STAGE_FIRST 0  // 1: dispatch the band-1 stage workgroups first (A/B)
-#endif
 // Band-0 fill and band-1 stage in one launch: workgroups [0, nfill) fill,
 // the rest stage, so the request-bound scattered stores of the one and the
 // latency-bound staging of the other share the CUs (and neither pays a tail).
@@ -1536,40 +1530,12 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_fill_stage_kernel(
     const uint32_t* __restrict__ cols, const uint32_t* __restrict__ start, uint32_t* __restrict__ entries,
     uint64_t cap, uint32_t* __restrict__ tmp, uint32_t nsup, uint32_t nfill) {
   extern __shared__ uint32_t sm[];
-#if DSE_BK_STAGE_FIRST
-  const uint32_t n1 = gridDim.x - nfill;
-  const uint32_t x = blockIdx.x < n1 ? nfill + blockIdx.x : blockIdx.x - n1;
-#else
   const uint32_t x = blockIdx.x;
-#endif
   if (x < nfill)
     bucket_fill_wg(sm, x, table, ba, range, cols, start, entries, cap);
   else
     bucket_stage_wg(sm, x - nfill, table, ba, range, cols, start, tmp, nsup);
 }
-
-#if DSE_BK_SORT_PEERS
-// Lanes of the wave whose key (< 2^bits) equals this lane's, among `valid` lanes.
-__device__ __forceinline__ uint64_t key_peers(uint32_t key, bool valid, uint32_t bits) {
-  uint64_t m = __ballot(valid);
-  for (uint32_t b = 0; b < bits; ++b) {
-    const bool set = (key >> b) & 1u;
-    const uint64_t x = __ballot(set);
-    m &= set ? x : ~x;
-  }
-  return m;
-}
-
-// LDS counter += number of peers; returns this lane's slot (old value + rank among its peers).
-__device__ __forceinline__ uint32_t peer_add(uint32_t* ctr, uint64_t peers, bool valid) {
-  const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(peers >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)peers, 0u));
-  uint32_t base = 0;
-  if (valid && rank == 0) base = atomicAdd(ctr, (uint32_t)__popcll(peers));
-  const uint32_t leader = valid ? (uint32_t)__builtin_ctzll(peers) : 0u;
-  base = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(leader << 2), (int)base);
-  return base + rank;
-}
-#endif
 
 __global__ __launch_bounds__(kSortThreads) void bucket_sort_kernel(BucketArgs ba, const uint32_t* __restrict__ cols,
                                                                    const uint32_t* __restrict__ start,
@@ -1619,15 +1585,7 @@ __global__ __launch_bounds__(kSortThreads) void bucket_sort_kernel(BucketArgs ba
     if (base + kSortTile < r1) load_tile(base + kSortTile);
 #pragma unroll
     for (uint32_t q = 0; q < kPer; ++q)
-#if DSE_BK_SORT_PEERS
-    {
-      const bool v = q * kSortThreads + tid < n;
-      const uint32_t k = key[q] >> kKeyShift;
-      rk[q] = peer_add(&hist[k], key_peers(k, v, kSupLog), v);
-    }
-#else
       rk[q] = q * kSortThreads + tid < n ? atomicAdd(&hist[key[q] >> kKeyShift], 1u) : 0u;
-#endif
     __syncthreads();
     if (tid < 64) {  // exclusive scan of the segment counts (one wave, kPerLane each)
       uint32_t c[kPerLane], sum = 0;
