@@ -27,5 +27,5 @@ run pmc_write --pmc WRITE_SIZE || exit 1
 for n in sq wait fetch write; do
   cp "$(find $OUT/pmc_$n -name '*counter_collection.csv' | head -1)" $OUT/summary/pmc_${n}_sieve_kernel.csv
 done
-grep -h "" $OUT/trace.log | tail -1 > $OUT/summary/bench_under_trace.json
+grep -h "^{\"metric\"" $OUT/trace.log | tail -1 > $OUT/summary/bench_under_trace.json
 echo done
