@@ -419,3 +419,6 @@ def test_debug_option_rejects_unknown(ctx):
     from mail_sieve_e import _dse
     with pytest.raises(_dse.DseError):
         ctx.debug_set_option("no_such_option", 1)
+    for name, bad in (("bucket_split_log2", 64), ("bucket_split_log2", -1), ("bucket_pass_segments", -1)):
+        with pytest.raises(_dse.DseError):
+            ctx.debug_set_option(name, bad)
