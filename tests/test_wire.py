@@ -217,9 +217,12 @@ def test_wire_follower_gpu(oracle, tmp_path):
     _mixed_ref_lead(oracle, tmp_path, None, n=400_000, P=3)
 
 
-def _silent_lead(port, behaviour):
-    """A lead that accepts one follower and then `behaviour(conn)`."""
-    srv = socket.create_server(("127.0.0.1", port))
+def _silent_lead(behaviour):
+    """A lead that accepts one follower and then `behaviour(conn)`; listens on
+    a port of its own choosing (bound here, so no other test can take it
+    between a free-port probe and the bind) and returns (thread, port)."""
+    srv = socket.create_server(("127.0.0.1", 0))
+    port = srv.getsockname()[1]
     def go():
         c, _ = srv.accept()
         try:
@@ -229,22 +232,20 @@ def _silent_lead(port, behaviour):
             srv.close()
     t = threading.Thread(target=go, daemon=True)
     t.start()
-    return t
+    return t, port
 
 
 def test_wire_follower_finite_timeout_is_a_protocol_error(oracle):
     """A finite timeout (tests only; the default waits forever like the
     reference) ends in a RuntimeError naming the wait, not queue.Empty."""
-    port = _free_port()
-    t = _silent_lead(port, lambda c: time.sleep(3))
+    t, port = _silent_lead(lambda c: time.sleep(3))
     with pytest.raises(RuntimeError, match="within"):
         wire.client_start("127.0.0.1", port, sieve_fn=_oracle_fn(oracle), timeout_s=0.5, write_file=False)
     t.join(5)
 
 
 def test_wire_follower_eof_before_number(oracle):
-    port = _free_port()
-    t = _silent_lead(port, lambda c: None)  # closes at once
+    t, port = _silent_lead(lambda c: None)  # closes at once
     with pytest.raises(RuntimeError, match="machine number"):
         wire.client_start("127.0.0.1", port, sieve_fn=_oracle_fn(oracle), write_file=False)
     t.join(5)
