@@ -215,8 +215,9 @@ def client_start(host: str, port: int, *, out_dir: Optional[str] = None, sieve_f
     if sieve_fn is None:
         sieve_fn, close = gpu_sieve_fn(device)
     print("connecting to host...", flush=True)
-    ch = LineChannel(socket.create_connection((host, port), timeout=timeout_s))
-    ch.sock.settimeout(None)
+    sock = socket.create_connection((host, port), timeout=timeout_s)
+    sock.settimeout(None)  # before the reader starts: a socket timeout there would read as the lead's EOF
+    ch = LineChannel(sock)
     try:
         my_num = _expect(ch, "the machine number", timeout_s)   # core.clj:188
         if not isinstance(my_num, int):

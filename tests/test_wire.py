@@ -238,9 +238,13 @@ def _silent_lead(behaviour):
 def test_wire_follower_finite_timeout_is_a_protocol_error(oracle):
     """A finite timeout (tests only; the default waits forever like the
     reference) ends in a RuntimeError naming the wait, not queue.Empty."""
-    t, port = _silent_lead(lambda c: time.sleep(3))
-    with pytest.raises(RuntimeError, match="within"):
-        wire.client_start("127.0.0.1", port, sieve_fn=_oracle_fn(oracle), timeout_s=0.5, write_file=False)
+    done = threading.Event()  # the lead stays silent until the client has given up (a fixed sleep
+    t, port = _silent_lead(lambda c: done.wait(60))  # raced the 0.5 s wait on a loaded host)
+    try:
+        with pytest.raises(RuntimeError, match="within"):
+            wire.client_start("127.0.0.1", port, sieve_fn=_oracle_fn(oracle), timeout_s=0.5, write_file=False)
+    finally:
+        done.set()
     t.join(5)
 
 
