@@ -62,35 +62,52 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(max_n: int) -> dict:
+def cpu_baseline(max_n: int, reps: int = 3) -> dict:
     """The reference's lead + followers on this host's cores (SURVEY.md 8(d)
     fallback: no JVM in the image): oracle/dse_oracle.c ref_sieve_threaded,
     P machine threads + machine 1's relay thread exchanging [mi ps p]
-    messages through in-process queues, at P = 2 and 3 on the README (1e4) and
-    Run Lead.bat (1e6) workloads and up to max_n. Test infrastructure:
+    messages through in-process queues (core.clj:118-134, sieve.clj:131-172),
+    at P = 2 and 3 on the README (1e4) and Run Lead.bat (1e6) workloads and up
+    to max_n. Each (N, P) runs `reps` times and reports the median; the
+    calling thread is pinned to P + 1 cores of its allowed set for the run
+    (os.sched_setaffinity, inherited by the machine threads; restored after),
+    so the threads do not migrate across the box's cores. Test infrastructure:
     reported only, never the measured path."""
     from oracle import oracle as o
     o.lib()
+    allowed = sorted(os.sched_getaffinity(0))
     runs = []
     ns = [n for n in (10**4, 10**6, 10**7, 10**8, 10**9) if n <= max_n]
-    for n in ns:
-        for P in (2, 3):
-            t = time.perf_counter()
-            _, _, counts, msgs = o.sieve_threaded(n, P, want_masks=False)
-            dt = time.perf_counter() - t
-            if n in KNOWN_PI:
-                tail_g, tail_n = o.tail_range(n, P)
-                _, ct = o.fast_sieve_range(tail_g, tail_n, want_mask=False) if tail_n else (None, 0)
-                assert o.pi_ref(counts) + ct == KNOWN_PI[n], (n, P)
-            runs.append({"N": n, "P": P, "threads": P + 1, "seconds": dt, "integers_per_s": n / dt,
-                         "prime_messages": int(msgs)})
-    head = max((r for r in runs if r["P"] == 3), key=lambda r: r["N"])
-    return {"value": head["integers_per_s"], "unit": "integers/s", "cores": head["threads"], "kind": "port",
-            "nproc": os.cpu_count(),
-            "sample": f"N={head['N']:.0e}, P=3: oracle/dse_oracle.c ref_sieve_threaded, the reference's lead + "
-                      f"2 followers as 3 machine threads + the relay thread, per-prime [mi ps p] messages through "
-                      f"in-process queues ({head['prime_messages']} messages), {head['seconds']:.2f} s; "
-                      "the Clojure reference cannot run (no JVM in the image)",
+    try:
+        for n in ns:
+            for P in (2, 3):
+                cores = allowed[:P + 1]
+                os.sched_setaffinity(0, cores)
+                ts = []
+                for _ in range(reps):
+                    t = time.perf_counter()
+                    _, _, counts, msgs = o.sieve_threaded(n, P, want_masks=False)
+                    ts.append(time.perf_counter() - t)
+                    if n in KNOWN_PI:
+                        tail_g, tail_n = o.tail_range(n, P)
+                        _, ct = o.fast_sieve_range(tail_g, tail_n, want_mask=False) if tail_n else (None, 0)
+                        assert o.pi_ref(counts) + ct == KNOWN_PI[n], (n, P)
+                dt = statistics.median(ts)
+                runs.append({"N": n, "P": P, "threads": P + 1, "cores": cores, "seconds": dt,
+                             "seconds_all": ts, "integers_per_s": n / dt, "prime_messages": int(msgs)})
+    finally:
+        os.sched_setaffinity(0, allowed)
+    top = max(r["N"] for r in runs)
+    h2 = next(r for r in runs if r["N"] == top and r["P"] == 2)
+    h3 = next(r for r in runs if r["N"] == top and r["P"] == 3)
+    return {"value": h3["integers_per_s"], "unit": "integers/s", "cores": h3["threads"], "kind": "port",
+            "nproc": os.cpu_count(), "allowed_cores": len(allowed), "pinned_cores": h3["cores"],
+            "value_P2": h2["integers_per_s"], "value_P3": h3["integers_per_s"],
+            "sample": f"N={top:.0e}, P=3 (P=2 beside it as value_P2): oracle/dse_oracle.c ref_sieve_threaded, the "
+                      f"reference's lead + 2 followers as 3 machine threads + the relay thread pinned to cores "
+                      f"{h3['cores']} of {len(allowed)} allowed ({os.cpu_count()} on the host), per-prime [mi ps p] "
+                      f"messages through in-process queues ({h3['prime_messages']} messages), median of {reps} runs "
+                      f"{h3['seconds']:.2f} s; the Clojure reference cannot run (no JVM in the image)",
             "runs": runs}
 
 

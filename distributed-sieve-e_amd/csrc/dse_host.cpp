@@ -22,9 +22,11 @@
 namespace {
 
 thread_local std::string g_err;
+thread_local int32_t g_code = DSE_OK;
 
 int32_t fail(int32_t code, const std::string& msg) {
   g_err = msg;
+  g_code = code;
   return code;
 }
 
@@ -122,6 +124,22 @@ int32_t build_table(DevState& d, uint64_t limit) {
   return DSE_OK;
 }
 
+// Enqueue a copy of the sticky bucket-overflow flag on d.stream (before the
+// caller's stream sync); check_flag after the sync reports and clears it.
+int32_t fetch_flag(DevState& d, uint32_t* h) {
+  *h = 0;
+  if (d.scratch.flag) HIP_TRY(hipMemcpyAsync(h, d.scratch.flag, sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
+  return DSE_OK;
+}
+
+int32_t check_flag(DevState& d, uint32_t h) {
+  if (!h) return DSE_OK;
+  HIP_TRY(hipMemsetAsync(d.scratch.flag, 0, sizeof(uint32_t), d.stream));
+  HIP_TRY(hipStreamSynchronize(d.stream));
+  return fail(DSE_EINTERNAL, "bucketed pass exceeded its entry capacity on device " + std::to_string(d.device) +
+                                 "; the count and mask of this call are not valid");
+}
+
 int32_t free_resident(DevState& d) {
   for (auto& c : d.resident)
     if (c.dev_ptr) HIP_TRY(hipFree(c.dev_ptr));
@@ -192,6 +210,8 @@ extern "C" {
 const char* dse_version(void) { return "dse 0.1 gfx950"; }
 
 const char* dse_last_error(void) { return g_err.c_str(); }
+
+int32_t dse_last_status(void) { return g_code; }
 
 int32_t dse_device_count(void) {
   int n = 0;
@@ -355,7 +375,10 @@ int32_t sieve_range_host(dse_ctx* ctx, DevState& d, uint64_t g0, uint64_t nbits,
   HIP_TRY(hipMemcpyAsync(&c, d.counts, sizeof(c), hipMemcpyDeviceToHost, d.stream));
   if (mask_or_null && words)
     HIP_TRY(hipMemcpyAsync(mask_or_null, d.scratch_mask, words * 8, hipMemcpyDeviceToHost, d.stream));
+  uint32_t hf;
+  if ((rc = fetch_flag(d, &hf))) return rc;
   HIP_TRY(hipStreamSynchronize(d.stream));
+  if ((rc = check_flag(d, hf))) return rc;
   if (count) *count = c;
   return DSE_OK;
 }
@@ -442,9 +465,15 @@ int32_t dse_sieve_all(dse_ctx* ctx, int64_t n, int32_t P, uint64_t* per_chunk_co
   HIP_TRY(hipSetDevice(ctx->devs[0].device));
   HIP_TRY(hipMemcpyAsync(h.data(), ctx->devs[0].counts, nc * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                          ctx->devs[0].stream));
+  std::vector<uint32_t> hf(nd);
   for (int i = 0; i < nd; ++i) {
     HIP_TRY(hipSetDevice(ctx->devs[i].device));
+    if ((rc = fetch_flag(ctx->devs[i], &hf[i]))) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->devs[i].stream));
+  }
+  for (int i = 0; i < nd; ++i) {
+    HIP_TRY(hipSetDevice(ctx->devs[i].device));
+    if ((rc = check_flag(ctx->devs[i], hf[i]))) return rc;
   }
   uint64_t sum = 0;
   for (int32_t k = 0; k < P; ++k) {
@@ -506,11 +535,32 @@ int32_t dse_sieve_window(dse_ctx* ctx, uint64_t lo, uint64_t hi, uint64_t* count
   unsigned long long c = 0;
   HIP_TRY(hipSetDevice(ctx->devs[0].device));
   HIP_TRY(hipMemcpyAsync(&c, ctx->devs[0].counts, sizeof(c), hipMemcpyDeviceToHost, ctx->devs[0].stream));
+  std::vector<uint32_t> hf(nd);
   for (int i = 0; i < nd; ++i) {
     HIP_TRY(hipSetDevice(ctx->devs[i].device));
+    if ((rc = fetch_flag(ctx->devs[i], &hf[i]))) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->devs[i].stream));
   }
+  for (int i = 0; i < nd; ++i) {
+    HIP_TRY(hipSetDevice(ctx->devs[i].device));
+    if ((rc = check_flag(ctx->devs[i], hf[i]))) return rc;
+  }
   *count = c;
+  return DSE_OK;
+}
+
+int32_t dse_device_status(dse_ctx* ctx) {
+  if (!ctx) return fail(DSE_EINVAL, "null ctx");
+  int32_t rc;
+  for (auto& d : ctx->devs) {
+    if (!d.scratch.flag) continue;
+    HIP_TRY(hipSetDevice(d.device));
+    if (d.scratch.used) HIP_TRY(hipEventSynchronize(d.scratch.done));
+    uint32_t hf;
+    if ((rc = fetch_flag(d, &hf))) return rc;
+    HIP_TRY(hipStreamSynchronize(d.stream));
+    if ((rc = check_flag(d, hf))) return rc;
+  }
   return DSE_OK;
 }
 
@@ -525,6 +575,11 @@ int32_t dse_debug_set_option(dse_ctx* ctx, const char* name, int64_t value) {
   if (n == "bucket_split_log2") {
     if (value < 0 || value > 63) return fail(DSE_EINVAL, "bucket_split_log2 out of range");
     ctx->opts.bucket_split_log2 = (uint32_t)value;
+    return DSE_OK;
+  }
+  if (n == "bucket_cap_divisor") {
+    if (value < 0 || value > 0xFFFFFFFFll) return fail(DSE_EINVAL, "bucket_cap_divisor out of range");
+    ctx->opts.bucket_cap_div = (uint32_t)value;
     return DSE_OK;
   }
   return fail(DSE_EINVAL, "unknown option " + n);

@@ -55,13 +55,16 @@ constexpr uint64_t kBaseLimitMax = 2ull * 150u * 1024u * 8u + 1ull;  // 150 KiB 
 constexpr uint64_t kBigBaseLimitMax = (1ull << 31) - 1;
 
 // Device scratch of one context (bucketed pass of high-offset ranges). Grows
-// on demand, freed by free_scratch (dse_destroy). `stream` is the stream of
-// the last pass that used it: a grow or a pass on another stream first waits
-// for that stream.
+// on demand, freed by free_scratch (dse_destroy). `done` is recorded on the
+// stream of every pass after its last kernel that reads the buffer (any
+// stream, the null stream included): the next pass's stream waits on it
+// (hipStreamWaitEvent, no host block) and a grow or a free synchronises on it.
 struct Scratch {
   void* ptr = nullptr;
   uint64_t bytes = 0;
-  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;  // created on first use
+  bool used = false;          // `done` has been recorded since the last grow
+  uint32_t* flag = nullptr;   // device {sticky overflow, this pass's overflow} (bucket capacity)
 };
 hipError_t free_scratch(Scratch* s);
 
@@ -70,6 +73,7 @@ hipError_t free_scratch(Scratch* s);
 struct SieveOpts {
   uint32_t bucket_pass_segs = 0;  // > 0: cap the segments per bucket pass (multi-pass coverage)
   uint32_t bucket_split_log2 = 0; // > 0: bucketed primes <= 2^k filled one level, above two levels (0: production)
+  uint32_t bucket_cap_div = 0;    // > 1: divide the (rigorous) bucket entry capacity, to test the overflow flag
 };
 
 hipError_t launch_base_primes(uint64_t limit, void* table, uint32_t cap, hipStream_t stream);

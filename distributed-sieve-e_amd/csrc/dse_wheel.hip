@@ -146,7 +146,7 @@ struct WheelArgs {
   uint8_t v0q[kNQ];    // V0 mod q
   uint16_t v0g[kNG];   // V0 mod M_G (init tables)
   const uint32_t* bk_entries;  // bucketed hits of the primes > kWheelMaxPrime (or null):
-  const uint32_t* bk_start;    // segment s owns entries [bk_start[s], bk_start[s+1]), k | plane << 16
+  const uint32_t* bk_start;    // segment s owns entries [bk_start[s], bk_start[s+1]), k | plane << kWheelLogKP
 };
 
 __device__ __forceinline__ void lds_or(uint32_t* a, uint32_t v) {
@@ -1154,7 +1154,7 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
 // such a prime hits a 2 M-integer segment less than once, so instead of
 // visiting every (prime, segment) pair the kernels below walk each prime's
 // multiples p*m, gcd(m, 30) = 1, across the whole range once and file every
-// hit under its segment: k | plane << 16. Two identical walks: count (LDS
+// hit under its segment: k | plane << kWheelLogKP. Two identical walks: count (LDS
 // per-segment counters -> per-workgroup column), then fill (LDS cursors
 // seeded from the scanned columns). The wheel kernel ORs its segment's list.
 // ---------------------------------------------------------------------------
@@ -1335,9 +1335,16 @@ __global__ __launch_bounds__(256) void bucket_colscan_kernel(uint32_t* __restric
   }
 }
 
-// exclusive scan of the segment totals -> start[0..nseg]
+// exclusive scan of the segment totals -> start[0..nseg]. A total above the
+// entry capacity (a rigorous bound, so never expected) sets *flag: the fill,
+// stage and sort kernels of the pass then skip, every segment's list is left
+// empty (start[] all 0) and the pass's count gets bit 63 set, so neither an
+// out-of-bounds store nor a silently wrong count can result; the host entry
+// points report it as DSE_EINTERNAL (dse_device_status).
 __global__ __launch_bounds__(1024) void bucket_startscan_kernel(const uint32_t* __restrict__ tot, uint32_t nseg,
-                                                                uint32_t* __restrict__ start) {
+                                                                uint32_t* __restrict__ start, uint64_t cap,
+                                                                uint32_t* __restrict__ flag,
+                                                                unsigned long long* __restrict__ count) {
   __shared__ uint32_t s_scan[1024];
   const uint32_t tid = threadIdx.x;
   const uint32_t per = (nseg + 1023) / 1024;
@@ -1352,13 +1359,23 @@ __global__ __launch_bounds__(1024) void bucket_startscan_kernel(const uint32_t* 
     s_scan[tid] += x;
     __syncthreads();
   }
+  const bool over = s_scan[1023] > cap;  // s_scan[1023]: every thread sees the same total
   uint32_t run = s_scan[tid] - sum;
   for (uint32_t b = b0; b < b1; ++b) {
     const uint32_t t = tot[b];
-    start[b] = run;
+    start[b] = over ? 0u : run;
     run += t;
   }
-  if (tid == 1023) start[nseg] = s_scan[1023];
+  if (tid == 1023) {
+    start[nseg] = over ? 0u : s_scan[1023];
+    if (over) {
+      flag[1] = 1u;  // this pass (read by the kernels below)
+      flag[0] = 1u;  // sticky, cleared by dse_device_status
+      atomicOr(count, 1ull << 63);
+    } else {
+      flag[1] = 0u;
+    }
+  }
 }
 
 // Band 0, one-level fill: every hit is one dword store at its slot (an LDS
@@ -1528,8 +1545,9 @@ __device__ __forceinline__ void bucket_stage_wg(uint32_t* sm, uint32_t b, const 
 __global__ __launch_bounds__(kBucketThreads) void bucket_fill_stage_kernel(
     const void* __restrict__ table, BucketArgs ba, const uint32_t* __restrict__ range,
     const uint32_t* __restrict__ cols, const uint32_t* __restrict__ start, uint32_t* __restrict__ entries,
-    uint64_t cap, uint32_t* __restrict__ tmp, uint32_t nsup, uint32_t nfill) {
+    uint64_t cap, uint32_t* __restrict__ tmp, uint32_t nsup, uint32_t nfill, const uint32_t* __restrict__ flag) {
   extern __shared__ uint32_t sm[];
+  if (flag[1]) return;  // capacity overflow (bucket_startscan_kernel)
   const uint32_t x = blockIdx.x;
   if (x < nfill)
     bucket_fill_wg(sm, x, table, ba, range, cols, start, entries, cap);
@@ -1540,7 +1558,9 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_fill_stage_kernel(
 __global__ __launch_bounds__(kSortThreads) void bucket_sort_kernel(BucketArgs ba, const uint32_t* __restrict__ cols,
                                                                    const uint32_t* __restrict__ start,
                                                                    const uint32_t* __restrict__ tmp,
-                                                                   uint32_t* __restrict__ entries) {
+                                                                   uint32_t* __restrict__ entries,
+                                                                   const uint32_t* __restrict__ flag) {
+  if (flag[1]) return;  // capacity overflow (bucket_startscan_kernel)
   constexpr uint32_t kPer = kSortTile / kSortThreads;
   constexpr uint32_t kPerLane = kSupSegs / 64;  // scan: segment counts per lane of wave 0
   __shared__ uint32_t sorted[kSortTile];
@@ -1644,13 +1664,17 @@ extern "C" int dse_debug_timing(unsigned long long* out) {
 #endif
 
 hipError_t free_scratch(Scratch* s) {
-  if (!s || !s->ptr) return hipSuccess;
-  hipError_t e = s->stream ? hipStreamSynchronize(s->stream) : hipSuccess;
-  const hipError_t f = hipFree(s->ptr);
+  if (!s) return hipSuccess;
+  hipError_t e = s->used ? hipEventSynchronize(s->done) : hipSuccess;  // the last pass may still read it
+  const hipError_t f = s->ptr ? hipFree(s->ptr) : hipSuccess;
+  const hipError_t g = s->done ? hipEventDestroy(s->done) : hipSuccess;
+  if (s->flag) (void)hipFree(s->flag);
+  s->flag = nullptr;
   s->ptr = nullptr;
   s->bytes = 0;
-  s->stream = nullptr;
-  return e != hipSuccess ? e : f;
+  s->done = nullptr;
+  s->used = false;
+  return e != hipSuccess ? e : f != hipSuccess ? f : g;
 }
 
 namespace {
@@ -1722,19 +1746,36 @@ uint64_t bucket_cap(uint64_t span, double a, double b) {
 
 constexpr uint64_t kBucketMaxEntries = 1ull << 31;  // 8 GB of entries per pass
 
-// Grow the context's scratch to `bytes` for a pass on `stream`.
+// Grow the context's scratch to `bytes` for a pass on `stream`, ordered after
+// the previous pass whatever stream that ran on: a grow waits for it on the
+// host (the old buffer is freed), otherwise `stream` waits for its event.
 hipError_t ensure_scratch(Scratch* sc, uint64_t bytes, hipStream_t stream, char** out) {
   hipError_t e;
-  // another stream's passes may still read the buffer
-  if (sc->ptr && sc->stream != stream && sc->stream && (e = hipStreamSynchronize(sc->stream)) != hipSuccess) return e;
+  if (!sc->done && (e = hipEventCreateWithFlags(&sc->done, hipEventDisableTiming)) != hipSuccess) return e;
+  if (!sc->flag) {
+    if ((e = hipMalloc(&sc->flag, 2 * sizeof(uint32_t))) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(sc->flag, 0, 2 * sizeof(uint32_t), stream)) != hipSuccess) return e;
+  }
   if (sc->bytes < bytes) {
-    if ((e = free_scratch(sc)) != hipSuccess) return e;
+    if (sc->used && (e = hipEventSynchronize(sc->done)) != hipSuccess) return e;
+    if (sc->ptr && (e = hipFree(sc->ptr)) != hipSuccess) return e;
+    sc->ptr = nullptr;
+    sc->bytes = 0;
+    sc->used = false;
     if ((e = hipMalloc(&sc->ptr, bytes)) != hipSuccess) return e;
     sc->bytes = bytes;
+  } else if (sc->used && (e = hipStreamWaitEvent(stream, sc->done, 0)) != hipSuccess) {
+    return e;
   }
-  sc->stream = stream;
   *out = static_cast<char*>(sc->ptr);
   return hipSuccess;
+}
+
+// After the last kernel of a pass that reads the scratch.
+hipError_t release_scratch(Scratch* sc, hipStream_t stream) {
+  const hipError_t e = hipEventRecord(sc->done, stream);
+  if (e == hipSuccess) sc->used = true;
+  return e;
 }
 
 hipError_t launch_wheel(const void* table, const WheelArgs& wa, uint32_t* out, unsigned long long* count,
@@ -1778,7 +1819,8 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     ba.nseg = (uint32_t)ns;
     ba.vmax = vmax_p;
     const uint64_t root_p = isqrt64(vmax_p);
-    const uint64_t cap = bucket_cap(ba.span, (double)kWheelMaxPrime, (double)root_p);
+    uint64_t cap = bucket_cap(ba.span, (double)kWheelMaxPrime, (double)root_p);
+    if (opts && opts->bucket_cap_div > 1) cap /= opts->bucket_cap_div;  // test-only: force the overflow path
     ba.split = 1ull << (opts && opts->bucket_split_log2 ? opts->bucket_split_log2 : kBucketSplitLog);
     const bool band0 = ba.split > kWheelMaxPrime, band1 = ba.split < root_p;
     // scratch: [range 3][cols 2*grid*ns][tot ns][start ns+1][entries cap][band-1 level-1 keys cap]
@@ -1799,7 +1841,8 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
                        ba, range, cols);
     hipLaunchKernelGGL(bucket_colscan_kernel, dim3((uint32_t)((ns + 3) / 4)), dim3(256), 0, stream, cols,
                        (uint32_t)ns, tot);
-    hipLaunchKernelGGL(bucket_startscan_kernel, dim3(1), dim3(1024), 0, stream, tot, (uint32_t)ns, start);
+    hipLaunchKernelGGL(bucket_startscan_kernel, dim3(1), dim3(1024), 0, stream, tot, (uint32_t)ns, start, cap,
+                       scratch->flag, count);
     const uint32_t nsup = (uint32_t)((ns + kSupSegs - 1) >> kSupLog);
     const uint32_t nfill = band0 ? kBucketGrid : 0;
     const uint32_t lds_bytes = std::max(band0 ? 4 * (uint32_t)ns : 0u, band1 ? 4 * stage_lds_words(nsup) : 0u);
@@ -1808,10 +1851,10 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes)) != hipSuccess)
       return e;
     hipLaunchKernelGGL(bucket_fill_stage_kernel, dim3(nfill + (band1 ? kBucketGrid1 : 0)), dim3(kBucketThreads),
-                       lds_bytes, stream, table, ba, range, cols, start, ent, cap, tmp, nsup, nfill);
+                       lds_bytes, stream, table, ba, range, cols, start, ent, cap, tmp, nsup, nfill, scratch->flag);
     if (band1) {
       hipLaunchKernelGGL(bucket_sort_kernel, dim3(nsup * (kBucketGrid1 / kSortGroup)), dim3(kSortThreads), 0,
-                         stream, ba, cols, start, tmp, ent);
+                         stream, ba, cols, start, tmp, ent, scratch->flag);
     }
     if ((e = hipGetLastError()) != hipSuccess) return e;
     wa.bk_entries = ent;
@@ -1819,6 +1862,7 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     if ((e = launch_wheel(table, wa, out ? out + s0 * (kWheelOutBits / 32) : nullptr, count, num_cus, stream)) !=
         hipSuccess)
       return e;
+    if ((e = release_scratch(scratch, stream)) != hipSuccess) return e;
     s0 += ns;
   }
   return hipSuccess;

@@ -21,6 +21,7 @@ ERRORS = {
     -4: "DSE_ENOMEM",
     -5: "DSE_EIO",
     -6: "DSE_ERANGE",
+    -7: "DSE_EINTERNAL",
 }
 
 # name -> (restype, argtypes); every symbol include/dse.h declares.
@@ -30,6 +31,7 @@ _pi64, _pu64 = ctypes.POINTER(_i64), ctypes.POINTER(_u64)
 SIGNATURES = {
     "dse_version": (_cp, []),
     "dse_last_error": (_cp, []),
+    "dse_last_status": (_i32, []),
     "dse_device_count": (_i32, []),
     "dse_init": (_vp, [_i32]),
     "dse_init_device": (_vp, [_i32]),
@@ -51,6 +53,7 @@ SIGNATURES = {
     "dse_base_table_prime_bytes": (_u64, [_u64]),
     "dse_base_table_finish_dev_async": (_i32, [_vp, _u64, _vp, _u64, _vp]),
     "dse_sieve_range_dev_async": (_i32, [_vp, _vp, _u64, _u64, _vp, _vp, _vp]),
+    "dse_device_status": (_i32, [_vp]),
     "dse_debug_set_option": (_i32, [_vp, _cp, _i64]),
 }
 

@@ -34,7 +34,7 @@ class Context:
         L = lib()
         self._ptr = L.dse_init_device(device) if device is not None else L.dse_init(num_gpus)
         if not self._ptr:
-            raise _dse.DseError(-2, "dse_init", L.dse_last_error().decode(errors="replace"))
+            raise _dse.DseError(L.dse_last_status(), "dse_init", L.dse_last_error().decode(errors="replace"))
 
     @property
     def ptr(self):
@@ -97,6 +97,11 @@ class Context:
         cnt = ctypes.c_uint64()
         check(lib().dse_sieve_window(self.ptr, lo, hi, ctypes.byref(cnt)), "dse_sieve_window")
         return cnt.value
+
+    def device_status(self) -> None:
+        """Raise DseError (DSE_EINTERNAL) if a device pass of this context broke
+        an invariant since the last check (the *_dev_async calls report here)."""
+        check(lib().dse_device_status(self.ptr), "dse_device_status")
 
     def debug_set_option(self, name: str, value: int) -> None:
         """Test-only knob of this context (include/dse.h dse_debug_set_option)."""

@@ -352,10 +352,17 @@ def main(argv=None) -> int:
     --timeout SECONDS bounds every protocol wait (default: wait forever)."""
     import sys
     argv = list(sys.argv[1:] if argv is None else argv)
+    usage = "usage: lead: <num-comps> <num-primes> <port> | follower: <host> <port> [--timeout S]"
     timeout_s = None
     if "--timeout" in argv:
         i = argv.index("--timeout")
-        timeout_s = float(argv[i + 1])
+        try:
+            timeout_s = float(argv[i + 1])
+            if not timeout_s > 0:
+                raise ValueError(argv[i + 1])
+        except (IndexError, ValueError):
+            print(usage, file=sys.stderr)
+            return 2
         del argv[i:i + 2]
     if len(argv) == 3:
         c = lead_start(int(argv[0]), int(argv[1]), int(argv[2]), timeout_s=timeout_s)
@@ -364,8 +371,7 @@ def main(argv=None) -> int:
         c = client_start(argv[0], int(argv[1]), timeout_s=timeout_s)
         print(f"{c.n_primes} odd primes in [{c.lower}, {c.upper})", flush=True)
     else:
-        print("usage: lead: <num-comps> <num-primes> <port> | follower: <host> <port> [--timeout S]",
-              file=sys.stderr)
+        print(usage, file=sys.stderr)
         return 2
     return 0
 

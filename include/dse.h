@@ -39,6 +39,7 @@ extern "C" {
 #define DSE_ENOMEM -4   /* host or device allocation failed */
 #define DSE_EIO -5      /* file I/O */
 #define DSE_ERANGE -6   /* input outside the supported range */
+#define DSE_EINTERNAL -7 /* device-side invariant broken (bucket capacity overflow); result not valid */
 
 typedef struct dse_ctx dse_ctx;
 
@@ -47,6 +48,10 @@ const char *dse_version(void);
 
 /* Message of the last failed call on this thread ("" if none). */
 const char *dse_last_error(void);
+
+/* DSE_E* status of the last failed call on this thread (DSE_OK if none); for
+ * the entry points that return a pointer (dse_init, dse_init_device). */
+int32_t dse_last_status(void);
 
 /* Number of visible HIP devices (0 if none). */
 int32_t dse_device_count(void);
@@ -159,10 +164,17 @@ int32_t dse_base_table_finish_dev_async(dse_ctx *ctx, uint64_t limit, void *tabl
 /* Sieve odd indices [g_start, g_start+nbits) with a base table on the device:
  * mask_dev (ceil(nbits/64) uint64 words, or NULL) receives the prime bits,
  * *count_dev (device uint64) is INCREMENTED by the prime count (zero it
- * first). Asynchronous on stream. */
+ * first). Asynchronous on stream. A device-side failure (DSE_EINTERNAL: a
+ * bucket pass over its entry capacity, a rigorous bound, so never expected)
+ * sets bit 63 of *count_dev and is reported by dse_device_status. */
 int32_t dse_sieve_range_dev_async(dse_ctx *ctx, const void *table_dev, uint64_t g_start,
                                   uint64_t nbits, uint64_t *mask_dev, uint64_t *count_dev,
                                   void *stream);
+
+/* Wait for the context's last bucketed pass, then read and clear its
+ * device-side error flag: DSE_OK, or DSE_EINTERNAL if any pass since the last
+ * check overflowed. The blocking entry points check it themselves. */
+int32_t dse_device_status(dse_ctx *ctx);
 
 /* ---- Test-only ---------------------------------------------------------- */
 
@@ -170,8 +182,11 @@ int32_t dse_sieve_range_dev_async(dse_ctx *ctx, const void *table_dev, uint64_t 
  * environment variable; defaults are the production configuration):
  *   "bucket_pass_segments" = k > 0: bucketed passes of at most k segments
  *   (covers the multi-pass path on small windows); 0 = default.
- *   "bucket_split_log2" = k in 1..63: bucketed primes <= 2^k take the
- *   one-level fill, larger ones the two-level staged fill; 0 = default.
+ *   "bucket_split_log2" = k in 0..63: bucketed primes <= 2^k take the
+ *   one-level fill, larger ones the two-level staged fill; 0 = the default
+ *   split (2^25).
+ *   "bucket_cap_divisor" = d >= 0: divide each pass's bucket entry capacity
+ *   by d (> 1), forcing the overflow path (DSE_EINTERNAL); 0 or 1 = default.
  * DSE_EINVAL for an unknown name or a value out of range. */
 int32_t dse_debug_set_option(dse_ctx *ctx, const char *name, int64_t value);
 

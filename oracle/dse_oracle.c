@@ -305,13 +305,17 @@ typedef struct {
 typedef struct {
   ref_msg *buf;
   size_t head, tail, cap;
+  int closed; /* set by rq_close: pops of an empty queue return REF_MSG_CLOSED */
   pthread_mutex_t mu;
   pthread_cond_t cv;
 } ref_queue;
 
+static const ref_msg REF_MSG_CLOSED = {-2, -2, 0};
+
 static int rq_init(ref_queue *q) {
   q->cap = 1024;
   q->head = q->tail = 0;
+  q->closed = 0;
   q->buf = (ref_msg *)malloc(q->cap * sizeof(ref_msg));
   if (!q->buf) return REF_ENOMEM;
   pthread_mutex_init(&q->mu, NULL);
@@ -348,10 +352,17 @@ static int rq_push(ref_queue *q, ref_msg m) {
 
 static ref_msg rq_pop(ref_queue *q) {
   pthread_mutex_lock(&q->mu);
-  while (q->head == q->tail) pthread_cond_wait(&q->cv, &q->mu);
-  ref_msg m = q->buf[q->head++];
+  while (q->head == q->tail && !q->closed) pthread_cond_wait(&q->cv, &q->mu);
+  const ref_msg m = q->head < q->tail ? q->buf[q->head++] : REF_MSG_CLOSED;
   pthread_mutex_unlock(&q->mu);
   return m;
+}
+
+static void rq_close(ref_queue *q) {
+  pthread_mutex_lock(&q->mu);
+  q->closed = 1;
+  pthread_cond_broadcast(&q->cv);
+  pthread_mutex_unlock(&q->mu);
 }
 
 typedef struct ref_run ref_run;
@@ -367,8 +378,35 @@ struct ref_run {
   ref_queue *q;   /* q[0] = relay (machine 1's transfer-primes), q[k-1] = machine k */
   uint64_t nmsg;  /* prime messages (all leads) */
   pthread_mutex_t nmsg_mu;
-  int err;
+  int err;        /* first failure (under nmsg_mu); non-zero closes every queue */
 };
+
+/* A failed push, thread start or invariant: record the first error and close
+ * every queue, so each machine and the relay return instead of waiting for a
+ * message that will never come. */
+static void ref_fail(ref_run *r, int code) {
+  pthread_mutex_lock(&r->nmsg_mu);
+  if (!r->err) r->err = code;
+  pthread_mutex_unlock(&r->nmsg_mu);
+  for (int32_t k = 0; k < r->P; ++k) rq_close(&r->q[k]);
+}
+
+static int ref_failed(ref_run *r) {
+  pthread_mutex_lock(&r->nmsg_mu);
+  const int e = r->err;
+  pthread_mutex_unlock(&r->nmsg_mu);
+  return e;
+}
+
+/* Send a lead's message to machines 2..P (machine 1) or to the relay. */
+static int ref_send(ref_run *r, int64_t m, ref_msg msg) {
+  if (m == 1) {
+    for (int64_t k = 2; k <= r->P; ++k)
+      if (rq_push(&r->q[k - 1], msg)) return REF_ENOMEM;
+    return REF_OK;
+  }
+  return rq_push(&r->q[0], msg);
+}
 
 /* Lead phase of machine m (sieve.clj:131-150). */
 static void ref_lead(ref_run *r, int64_t m) {
@@ -379,23 +417,16 @@ static void ref_lead(ref_run *r, int64_t m) {
   for (;;) {
     int64_t n_start = ref_find_next_non_zero(own, start, cs);
     if (n_start < 0) break;
-    if (start >= cs || own[start] == 0) { r->err = REF_EINTERNAL; break; }
+    if (start >= cs || own[start] == 0) { ref_fail(r, REF_EINTERNAL); return; }
     ref_msg msg = {m, start, 3 + 2 * ((m - 1) * cs + start)};
-    if (m == 1) {
-      for (int64_t k = 2; k <= r->P; ++k) rq_push(&r->q[k - 1], msg);
-    } else {
-      rq_push(&r->q[0], msg);
-    }
+    if (ref_send(r, m, msg)) { ref_fail(r, REF_ENOMEM); return; }
     ++sent;
     ref_mark_composites(m, cs, start, msg.p, m, own);
     start = n_start;
+    if ((sent & 1023) == 0 && ref_failed(r)) return;
   }
   ref_msg appoint = {m, -1, 0};
-  if (m == 1) {
-    for (int64_t k = 2; k <= r->P; ++k) rq_push(&r->q[k - 1], appoint);
-  } else {
-    rq_push(&r->q[0], appoint);
-  }
+  if (ref_send(r, m, appoint)) { ref_fail(r, REF_ENOMEM); return; }
   pthread_mutex_lock(&r->nmsg_mu);
   r->nmsg += sent;
   pthread_mutex_unlock(&r->nmsg_mu);
@@ -409,6 +440,7 @@ static void *ref_machine_main(void *arg) {
   if (m > 1) {
     for (;;) { /* follower loop, sieve.clj:154-171 */
       ref_msg msg = rq_pop(&r->q[m - 1]);
+      if (msg.mi == REF_MSG_CLOSED.mi) return NULL; /* the run failed elsewhere */
       if (msg.ps == -1) {
         if (msg.mi == m - 1) break; /* appointed */
         continue;
@@ -425,7 +457,9 @@ static void *ref_relay_main(void *arg) {
   ref_run *r = (ref_run *)arg;
   for (;;) {
     ref_msg msg = rq_pop(&r->q[0]);
-    for (int64_t k = msg.mi + 1; k <= r->P; ++k) rq_push(&r->q[k - 1], msg);
+    if (msg.mi == REF_MSG_CLOSED.mi) return NULL;
+    for (int64_t k = msg.mi + 1; k <= r->P; ++k)
+      if (rq_push(&r->q[k - 1], msg)) { ref_fail(r, REF_ENOMEM); return NULL; }
     if (msg.ps == -1 && msg.mi == r->P) break;
   }
   return NULL;
@@ -448,16 +482,30 @@ int ref_sieve_threaded(int64_t n, int32_t P, uint64_t *masks, uint64_t *counts, 
   pthread_t *th = (pthread_t *)calloc((size_t)P + 1, sizeof(pthread_t));
   if (!r.flags || !r.q || !mc || !th) { free(r.flags); free(r.q); free(mc); free(th); return REF_ENOMEM; }
   memset(r.flags, 1, (size_t)P * (size_t)cs); /* gen-table */
+  int32_t nq = 0;
+  while (nq < P && rq_init(&r.q[nq]) == REF_OK) ++nq;
+  if (nq < P) {
+    for (int32_t k = 0; k < nq; ++k) rq_free(&r.q[k]);
+    free(r.flags); free(r.q); free(mc); free(th);
+    return REF_ENOMEM;
+  }
   pthread_mutex_init(&r.nmsg_mu, NULL);
-  for (int32_t k = 0; k < P; ++k) rq_init(&r.q[k]);
-  for (int32_t k = 0; k < P; ++k) {
+  /* st[k]: thread k is running and must be joined (st[P] = the relay) */
+  uint8_t *st = (uint8_t *)calloc((size_t)P + 1, 1);
+  if (!st) ref_fail(&r, REF_ENOMEM);
+  for (int32_t k = 0; st && k < P; ++k) {
     mc[k].run = &r;
     mc[k].my_num = k + 1;
-    pthread_create(&th[k], NULL, ref_machine_main, &mc[k]);
+    if (pthread_create(&th[k], NULL, ref_machine_main, &mc[k]) != 0) { ref_fail(&r, REF_EINTERNAL); break; }
+    st[k] = 1;
   }
-  if (P > 1) pthread_create(&th[P], NULL, ref_relay_main, &r);
-  for (int32_t k = 0; k < P; ++k) pthread_join(th[k], NULL);
-  if (P > 1) pthread_join(th[P], NULL);
+  if (st && P > 1 && !ref_failed(&r)) {
+    if (pthread_create(&th[P], NULL, ref_relay_main, &r) != 0) ref_fail(&r, REF_EINTERNAL);
+    else st[P] = 1;
+  }
+  for (int32_t k = 0; st && k <= P; ++k)
+    if (st[k]) pthread_join(th[k], NULL);
+  free(st);
   rc = r.err;
   if (!rc) {
     int64_t words = (cs + 63) / 64;

@@ -112,10 +112,14 @@ def test_chunks_concatenate_to_single_chunk(ctx):
         assert not bk[cs:].any()  # tail bits of the last word are zero
 
 
-def _chunk_sha_streamed(ctx, N, P, k):
-    """SHA-256 of chunk k's resident mask (dse_copy_chunk_mask), hashed as it
-    is copied back."""
-    return sha(ctx.copy_chunk_mask(N, P, k))
+def _chunk_sha_resident(ctx, N, P, k):
+    """SHA-256 of chunk k's resident mask (dse_copy_chunk_mask): one host copy
+    (up to 7.8 GB at 1e12 P=8), hashed in place through its buffer, no second
+    copy."""
+    m = ctx.copy_chunk_mask(N, P, k)
+    h = hashlib.sha256(memoryview(m).cast("B")).hexdigest()
+    del m
+    return h
 
 
 @pytest.mark.parametrize("P", [1, 2, 4, 8])
@@ -128,7 +132,7 @@ def test_1e11_chunks_golden(ctx, P):
     assert pi_ref == pi_full == 4_118_054_813 == g["pi_full"]
     assert [int(x) for x in counts] == g["counts"]
     for k in range(P):
-        assert _chunk_sha_streamed(ctx, 10**11, P, k + 1) == g["mask_sha256"][k], (P, k + 1)
+        assert _chunk_sha_resident(ctx, 10**11, P, k + 1) == g["mask_sha256"][k], (P, k + 1)
 
 
 def test_pi_1e12_dropped_tail(ctx):
@@ -142,7 +146,7 @@ def test_pi_1e12_dropped_tail(ctx):
     if g is not None:
         assert [int(x) for x in counts] == g["counts"]
         for k in range(8):
-            assert _chunk_sha_streamed(ctx, 10**12, 8, k + 1) == g["mask_sha256"][k], k + 1
+            assert _chunk_sha_resident(ctx, 10**12, 8, k + 1) == g["mask_sha256"][k], k + 1
 
 
 def test_idempotent(ctx):
@@ -419,6 +423,85 @@ def test_debug_option_rejects_unknown(ctx):
     from mail_sieve_e import _dse
     with pytest.raises(_dse.DseError):
         ctx.debug_set_option("no_such_option", 1)
-    for name, bad in (("bucket_split_log2", 64), ("bucket_split_log2", -1), ("bucket_pass_segments", -1)):
+    for name, bad in (("bucket_split_log2", 64), ("bucket_split_log2", -1), ("bucket_pass_segments", -1),
+                      ("bucket_cap_divisor", -1)):
         with pytest.raises(_dse.DseError):
             ctx.debug_set_option(name, bad)
+
+
+def test_bucket_overflow_flag(oracle):
+    """A bucketed pass over its entry capacity (forced with the test-only
+    option bucket_cap_divisor; the production bound is rigorous) must fail
+    loudly: DSE_EINTERNAL from the blocking entry points, bit 63 of the device
+    count plus DSE_EINTERNAL from dse_device_status on the async path, and no
+    stale flag once the option is cleared."""
+    import torch
+    from mail_sieve_e import _dse
+    from mail_sieve_e import sieve as S
+    g0, nb = (10**13 + 1 - 3) // 2, 5 * 10**6
+    m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
+    with S.Context(num_gpus=1) as c:
+        c.debug_set_option("bucket_cap_divisor", 1000)
+        with pytest.raises(_dse.DseError) as e:
+            c.sieve_odd_range(g0, nb)
+        assert e.value.code == -7 and "capacity" in str(e.value)
+        with pytest.raises(_dse.DseError) as e:
+            c.sieve_window(10**18, 10**18 + 10**7)
+        assert e.value.code == -7
+        limit = S.base_limit_for_range(g0, nb)
+        table = torch.empty(S.base_table_bytes(limit), dtype=torch.uint8, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        sp = torch.cuda.current_stream().cuda_stream
+        c.base_primes_dev_async(limit, table.data_ptr(), table.numel(), sp)
+        c.sieve_range_dev_async(table.data_ptr(), g0, nb, 0, cnt.data_ptr(), sp)
+        torch.cuda.synchronize()
+        assert int(cnt.item()) < 0  # bit 63
+        with pytest.raises(_dse.DseError) as e:
+            c.device_status()
+        assert e.value.code == -7
+        c.device_status()  # cleared
+        c.debug_set_option("bucket_cap_divisor", 0)
+        m, cnt2 = c.sieve_odd_range(g0, nb)
+        assert cnt2 == c_ref and np.array_equal(m, m_ref)
+
+
+def test_scratch_null_stream_then_host_call(oracle):
+    """a bucketed pass on the null stream (dev_async, stream 0)
+    followed at once by a host entry point on the same context (its own
+    non-blocking stream, the same scratch): the second pass waits for the
+    first (event-ordered scratch), both bit-exact."""
+    import torch
+    from mail_sieve_e import sieve as S
+    g0a, nba = (10**15 + 1 - 3) // 2, 3 * 10**7
+    g0b, nbb = (10**14 + 1 - 3) // 2, 2 * 10**7
+    ra, rb = oracle.fast_sieve_range(g0a, nba), oracle.fast_sieve_range(g0b, nbb)
+    with S.Context(num_gpus=1) as c:
+        limit = S.base_limit_for_range(g0a, nba)
+        table = torch.empty(S.base_table_bytes(limit), dtype=torch.uint8, device="cuda")
+        mask = torch.zeros((nba + 63) // 64, dtype=torch.int64, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        for _ in range(3):
+            cnt.zero_()
+            torch.cuda.synchronize()
+            c.base_primes_dev_async(limit, table.data_ptr(), table.numel(), 0)
+            c.sieve_range_dev_async(table.data_ptr(), g0a, nba, mask.data_ptr(), cnt.data_ptr(), 0)
+            m, cb = c.sieve_odd_range(g0b, nbb)  # no host sync in between
+            assert cb == rb[1] and np.array_equal(m, rb[0])
+            torch.cuda.synchronize()
+            assert int(cnt.item()) == ra[1]
+            assert np.array_equal(mask.cpu().numpy().view(np.uint64), ra[0])
+        c.device_status()
+
+
+def test_init_more_devices_than_visible():
+    """dse_init(n) with n above the visible devices: DSE_EINVAL, a message
+    naming both numbers, no context (the single-process multi-GPU path,
+    core.clj:141-147's wait for clients, must refuse rather than hang)."""
+    import torch
+    from mail_sieve_e import _dse
+    from mail_sieve_e import sieve as S
+    n = torch.cuda.device_count()
+    with pytest.raises(_dse.DseError) as e:
+        S.Context(num_gpus=n + 1)
+    assert e.value.code == -1
+    assert f"asked for {n + 1} GPUs, {n} visible" in str(e.value)

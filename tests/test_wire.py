@@ -259,3 +259,13 @@ def test_wire_default_waits_are_unbounded():
     import inspect
     assert inspect.signature(wire.client_start).parameters["timeout_s"].default is None
     assert inspect.signature(wire.lead_start).parameters["timeout_s"].default is None
+
+
+def test_main_rejects_bad_timeout(capsys):
+    """-main's optional --timeout: missing or non-positive values print the
+    usage line and return 2 instead of raising."""
+    from mail_sieve_e import wire
+    for argv in (["localhost", "1", "--timeout"], ["localhost", "1", "--timeout", "abc"],
+                 ["--timeout", "-3", "localhost", "1"], ["just-one-arg"]):
+        assert wire.main(argv) == 2, argv
+        assert "usage:" in capsys.readouterr().err
