@@ -577,6 +577,11 @@ int32_t dse_debug_set_option(dse_ctx* ctx, const char* name, int64_t value) {
     ctx->opts.bucket_split_log2 = (uint32_t)value;
     return DSE_OK;
   }
+  if (n == "wheel_geometry") {
+    if (value < 0 || value > 2) return fail(DSE_EINVAL, "wheel_geometry must be 0, 1 or 2");
+    ctx->opts.wheel_geometry = (uint32_t)value;
+    return DSE_OK;
+  }
   if (n == "bucket_cap_divisor") {
     if (value < 0 || value > 0xFFFFFFFFll) return fail(DSE_EINVAL, "bucket_cap_divisor out of range");
     ctx->opts.bucket_cap_div = (uint32_t)value;

@@ -74,6 +74,7 @@ struct SieveOpts {
   uint32_t bucket_pass_segs = 0;  // > 0: cap the segments per bucket pass (multi-pass coverage)
   uint32_t bucket_split_log2 = 0; // > 0: bucketed primes <= 2^k filled one level, above two levels (0: production)
   uint32_t bucket_cap_div = 0;    // > 1: divide the (rigorous) bucket entry capacity, to test the overflow flag
+  uint32_t wheel_geometry = 0;    // ranges without buckets: 0 auto (half-size tail), 1 full only, 2 half only
 };
 
 hipError_t launch_base_primes(uint64_t limit, void* table, uint32_t cap, hipStream_t stream);
@@ -89,6 +90,11 @@ hipError_t launch_base_primes_big(uint64_t limit, void* table, uint32_t cap, int
 hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
                               unsigned long long* count, int num_cus, hipStream_t stream, Scratch* scratch,
                               const SieveOpts* opts);
+// The same sieve with the half-size segment geometry (2^16 periods,
+// dse_wheel_half.hip): launch_sieve_range gives it the tail of a range whose
+// last round of full segments would leave most CUs idle. No bucketed primes.
+hipError_t launch_wheel_range_half(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
+                                   unsigned long long* count, int num_cus, hipStream_t stream);
 // Fill the Barrett factors m[] and wheel offsets a[] of a table whose p[] is final.
 // n_hint: table capacity when known (sizes the grid: about 4 primes per thread)
 hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream, uint64_t n_hint = 0);

@@ -45,6 +45,8 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <array>
+#include <vector>
 
 #include "dse_internal.h"
 
@@ -74,6 +76,18 @@ static_assert(NE >= 1 && NE <= NW && (DSE_PIPELINE ? NE < NW : NE == NW) && ROWS
               "expander rows");
 #ifndef DSE_TA
 #define DSE_TA 256
+#endif
+#ifndef DSE_L_SETS
+#define DSE_L_SETS 1  // sets of 64 primes per L unit (A/B)
+#endif
+#ifndef DSE_WHEEL_HALF_TU
+#define DSE_WHEEL_HALF_TU 0  // 1: compiled by dse_wheel_half.hip with 2^16 periods per segment
+#endif
+#ifndef DSE_HALF_SEG_COST
+#define DSE_HALF_SEG_COST 0.68
+#endif
+#ifndef DSE_LAUNCH_COST
+#define DSE_LAUNCH_COST 0.5
 #endif
 constexpr uint32_t TA = DSE_TA;             // A/B threshold
 #ifndef DSE_TB
@@ -134,6 +148,31 @@ constexpr uint32_t kGInv30[kNG] = {inv30_const(gmod(0)), inv30_const(gmod(1)), i
                                    inv30_const(gmod(3)), inv30_const(gmod(4)), inv30_const(gmod(5)),
                                    inv30_const(gmod(6))};
 
+#if !DSE_INIT_REGS
+// The init tables, built at compile time (a launch copies them into LDS):
+// copy k, group g, dword gbase(g) + j = bits [32 (j + k), 32 (j + k) + 32) of U_g.
+struct InitTables {
+  uint32_t w[4 * kGDW];
+};
+constexpr InitTables make_init_tables() {
+  InitTables t{};
+  for (int g = 0; g < kNG; ++g) {
+    for (uint32_t j = 0; j < gdw(g) + 3; ++j) {  // dword j of U_g
+      uint32_t v = 0;
+      for (uint32_t b = 0; b < 32; ++b) {
+        const uint32_t y = 32 * j + b;
+        const bool hit = y % kGQ[g][0] == 0 || y % kGQ[g][1] == 0 || (kGQ[g][2] > 1 && y % kGQ[g][2] == 0);
+        v |= (uint32_t)hit << b;
+      }
+      for (uint32_t k = 0; k < 4; ++k)
+        if (j >= k && j - k < gdw(g)) t.w[k * kGDW + gbase(g) + (j - k)] = v;
+    }
+  }
+  return t;
+}
+__device__ const InitTables g_init_tables = make_init_tables();
+#endif
+
 struct WheelArgs {
   uint64_t V0;         // v_start - 1
   uint64_t nbits;      // odd candidates in the range
@@ -145,6 +184,7 @@ struct WheelArgs {
   uint32_t phases;
   uint8_t v0q[kNQ];    // V0 mod q
   uint16_t v0g[kNG];   // V0 mod M_G (init tables)
+  uint32_t nthr[4];    // odd primes <= 61, <= TA, <= TB, <= kWheelMaxPrime (table indices of the unit lists)
   const uint32_t* bk_entries;  // bucketed hits of the primes > kWheelMaxPrime (or null):
   const uint32_t* bk_start;    // segment s owns entries [bk_start[s], bk_start[s+1]), k | plane << kWheelLogKP
 };
@@ -516,11 +556,22 @@ __device__ __forceinline__ void load_L(LargeOps& o, const uint32_t* __restrict__
 // The masks keep any kk inside the image, so a predicated-off mark (PRED and
 // kk >= KP) is an OR of 0 at a valid address. asm for the same reason as
 // mark_col.
+#ifndef DSE_PRED_EXEC
+#define DSE_PRED_EXEC 0  // 1: predicated-off marks leave the instruction (exec mask) instead of ORing 0 (A/B)
+#endif
 template <bool PRED>
 __device__ __forceinline__ void mark_plane(uint32_t pb4, uint32_t kk) {
+#if DSE_PRED_EXEC
+  // a lane without a hit takes no part in the ds_or, so it adds no bank
+  // conflict (an OR of 0 at a random column conflicts like a mark)
+  if (PRED && kk >= KP) return;
+  constexpr bool kOr0 = false;
+#else
+  constexpr bool kOr0 = PRED;
+#endif
   const uint32_t col = __builtin_amdgcn_ubfe(kk, LOG_LS, 3);
   uint32_t bit = 1u << (kk & 31);
-  if (PRED) bit = kk < KP ? bit : 0u;
+  if (kOr0) bit = kk < KP ? bit : 0u;
   uint32_t a, t;
   asm volatile(
       "v_lshl_or_b32 %1, %2, 5, %3\n\t"
@@ -723,20 +774,14 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
 #endif
 
   if (tid == 0) {
-    // first index with p > 61, with p > TA, with p > TB (capped by the LDS stage)
-    uint32_t lo = 0, hi = np;
-    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= kQMax) lo = mid + 1; else hi = mid; }
-    s_thr[0] = lo;
-    hi = np;
-    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= TA) lo = mid + 1; else hi = mid; }
-    s_thr[1] = lo;
-    hi = np;
-    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= TB) lo = mid + 1; else hi = mid; }
-    s_thr[2] = min(lo, s_thr[0] + kMidCap);
-    lo = s_thr[2];
-    hi = np;  // primes above kWheelMaxPrime are bucketed (or absent)
-    while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= kWheelMaxPrime) lo = mid + 1; else hi = mid; }
-    s_thr[3] = lo;
+    // first index with p > 61, with p > TA, with p > TB (capped by the LDS
+    // stage), with p > kWheelMaxPrime (bucketed or absent): the table holds
+    // every odd prime from 3 up, so these are the host's prime counts
+    // (wa.nthr), capped by the table's size
+    s_thr[0] = min(wa.nthr[0], np);
+    s_thr[1] = min(wa.nthr[1], np);
+    s_thr[2] = min(min(wa.nthr[2], np), s_thr[0] + kMidCap);
+    s_thr[3] = max(s_thr[2], min(wa.nthr[3], np));
     lds.ctr[0] = 0;
     lds.ctr[1] = 0;
   }
@@ -752,25 +797,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     s_lut[tid ^ (3u * (tid >> 5))] = v;
   }
 #if !DSE_INIT_REGS
-  // copy k, group g, dword i = bits [32 (i + k), 32 (i + k) + 32) of U_g
-  for (uint32_t idx = tid; idx < 4 * kGDW; idx += NT) {
-    const uint32_t k = idx / kGDW, i = idx - k * kGDW;
-    uint32_t v = 0;
-#pragma unroll
-    for (int g = 0; g < kNG; ++g) {
-      if (i >= gbase(g) && i < gbase(g) + gdw(g)) {
-        const uint32_t y0 = 32 * (i - gbase(g) + k);
-#pragma unroll 1
-        for (uint32_t b = 0; b < 32; ++b) {
-          const uint32_t y = y0 + b;
-          bool hit = y % kGQ[g][0] == 0 || y % kGQ[g][1] == 0;
-          if (kGQ[g][2] > 1) hit = hit || y % kGQ[g][2] == 0;
-          v |= (uint32_t)hit << b;
-        }
-      }
-    }
-    reinterpret_cast<uint32_t*>(lds.itab)[idx] = v;
-  }
+  for (uint32_t idx = tid; idx < 4 * kGDW; idx += NT) reinterpret_cast<uint32_t*>(lds.itab)[idx] = g_init_tables.w[idx];
 #endif
   __syncthreads();
   const uint32_t i_mid0 = s_thr[0], i_midB = s_thr[1], i_mid1 = s_thr[2];
@@ -788,7 +815,8 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   const uint32_t n_mid = i_mid1 - i_mid0;
   const uint32_t nB = (i_mid1 - i_midB + 7) / 8;
   const uint32_t i_big = s_thr[3];             // L units end here
-  const uint32_t nL = (i_big - i_mid1 + 63) / 64;
+  constexpr uint32_t kLU = 64 * DSE_L_SETS;  // primes per L unit
+  const uint32_t nL = (i_big - i_mid1 + kLU - 1) / kLU;
   const uint32_t n1 = nA + nB, n2 = nL;
 
   const uint64_t out_words = 2ull * ((wa.nbits + 63) / 64);  // 32-bit words of the caller's mask
@@ -1010,12 +1038,25 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     auto is_l = [&](uint32_t u) -> bool { return u < 2 * n_int ? (u & 1) != 0 : n2 > n1; };
     auto idx_of = [&](uint32_t u) -> uint32_t { return u < 2 * n_int ? u >> 1 : u - n_int; };
     LargeOps cur, nxt;
+#if DSE_L_SETS == 2
+    LargeOps cur1, nxt1;  // the unit's second 64 primes
+#endif
     uint32_t u_cur = claimed(claim());
     uint32_t u_nxt = claimed(claim());
-    if (u_cur < n_all && is_l(u_cur)) load_L(cur, P, M, A, i_mid1 + 64 * idx_of(u_cur) + lane, i_big);
+    if (u_cur < n_all && is_l(u_cur)) {
+      load_L(cur, P, M, A, i_mid1 + kLU * idx_of(u_cur) + lane, i_big);
+#if DSE_L_SETS == 2
+      load_L(cur1, P, M, A, i_mid1 + kLU * idx_of(u_cur) + 64 + lane, i_big);
+#endif
+    }
     while (u_cur < n_all) {
       const uint32_t c2 = claim();  // unit after next, read at the end of this one
-      if (u_nxt < n_all && is_l(u_nxt)) load_L(nxt, P, M, A, i_mid1 + 64 * idx_of(u_nxt) + lane, i_big);
+      if (u_nxt < n_all && is_l(u_nxt)) {
+        load_L(nxt, P, M, A, i_mid1 + kLU * idx_of(u_nxt) + lane, i_big);
+#if DSE_L_SETS == 2
+        load_L(nxt1, P, M, A, i_mid1 + kLU * idx_of(u_nxt) + 64 + lane, i_big);
+#endif
+      }
       const uint32_t k = idx_of(u_cur);
 #ifdef DSE_TIMING
       const uint64_t t_u0 = __builtin_amdgcn_s_memtime();
@@ -1037,12 +1078,19 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       } else {
         const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p);
         if ((phases & kPhaseLarge) && (uint64_t)p0 * p0 < Vend) unit_L(cur, Vs, Vend, Kb, ps, pl_rot, wa.rho_pack);
+#if DSE_L_SETS == 2
+        const uint32_t p1 = __builtin_amdgcn_readfirstlane(cur1.p);
+        if ((phases & kPhaseLarge) && (uint64_t)p1 * p1 < Vend) unit_L(cur1, Vs, Vend, Kb, ps, pl_rot, wa.rho_pack);
+#endif
       }
 #ifdef DSE_TIMING
       lds_drain();
       t_acc[u_type] += __builtin_amdgcn_s_memtime() - t_u0;
 #endif
       cur = nxt;
+#if DSE_L_SETS == 2
+      cur1 = nxt1;
+#endif
       u_cur = u_nxt;
       u_nxt = claimed(c2);
     }
@@ -1106,6 +1154,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   }
 }
 
+#if !DSE_WHEEL_HALF_TU
 // floor((2^64-1)/p) for 2 <= p < 2^32 without a 64-bit division: a double
 // quotient (relative error 2^-52, so off by < 2^11) corrected by the exact
 // remainder, itself below 2^43 in magnitude and so exact in a double.
@@ -1193,25 +1242,40 @@ struct BucketArgs {
   uint64_t split;      // band 0: kWheelMaxPrime < p <= split, band 1: p > split
 };
 
+// First index in [lo, hi) where the ascending table P has P[i] > bound (hi
+// if none), by one wave: 64 pivots per step (a step's loads are independent,
+// so a 50 M-prime table takes 4 dependent loads instead of 26).
+__device__ uint32_t wave_upper_bound(const uint32_t* __restrict__ P, uint32_t lo, uint32_t hi, uint64_t bound,
+                                     bool squared) {
+  const uint32_t lane = threadIdx.x & 63;
+  auto le = [&](uint32_t i) { const uint64_t p = P[i]; return (squared ? p * p : p) <= bound; };
+  while (hi - lo > 64) {
+    const uint32_t step = (hi - lo + 63) / 64, i = lo + lane * step;
+    const uint32_t c = (uint32_t)__popcll(__ballot(i < hi && le(i)));  // pivots at or below the bound
+    if (c == 0) return lo;
+    const uint32_t nhi = min(hi, lo + c * step);  // the answer is in (pivot c-1, pivot c]
+    lo += (c - 1) * step + 1;
+    hi = nhi;
+  }
+  return lo + (uint32_t)__popcll(__ballot(lo + lane < hi && le(lo + lane)));
+}
+
 // range[0] = first table index with p > kWheelMaxPrime, range[1] = first with
-// p^2 > vmax, range[2] = first with p > split (clamped to [range[0], range[1]])
-__global__ void bucket_range_kernel(const void* __restrict__ table, uint64_t vmax, uint64_t split,
-                                    uint32_t* __restrict__ range) {
+// p^2 > vmax, range[2] = first with p > split (clamped to [range[0], range[1]]).
+// One wave.
+__global__ __launch_bounds__(64) void bucket_range_kernel(const void* __restrict__ table, uint64_t vmax,
+                                                          uint64_t split, uint32_t* __restrict__ range) {
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
   const uint32_t np = th->count == 0xFFFFFFFFu ? 0u : th->count;
   const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
-  uint32_t lo = 0, hi = np;
-  while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= kWheelMaxPrime) lo = mid + 1; else hi = mid; }
-  range[0] = lo;
-  const uint32_t i_lo = lo;
-  hi = np;
-  while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if ((uint64_t)P[mid] * P[mid] <= vmax) lo = mid + 1; else hi = mid; }
-  range[1] = lo;
-  const uint32_t i_hi = lo;
-  lo = i_lo;
-  hi = i_hi;
-  while (lo < hi) { uint32_t mid = (lo + hi) >> 1; if (P[mid] <= split) lo = mid + 1; else hi = mid; }
-  range[2] = lo;
+  const uint32_t i_lo = wave_upper_bound(P, 0, np, kWheelMaxPrime, false);
+  const uint32_t i_hi = max(i_lo, wave_upper_bound(P, i_lo, np, vmax, true));
+  const uint32_t i_sp = wave_upper_bound(P, i_lo, i_hi, split, false);
+  if (threadIdx.x == 0) {
+    range[0] = i_lo;
+    range[1] = i_hi;
+    range[2] = i_sp;
+  }
 }
 
 // First coprime-to-30 multiple of p at or above max(V0 + 1, p^2): its offset
@@ -1646,8 +1710,10 @@ __global__ __launch_bounds__(kSortThreads) void bucket_sort_kernel(BucketArgs ba
   }
 }
 
+#endif  // !DSE_WHEEL_HALF_TU
 }  // namespace
 
+#if !DSE_WHEEL_HALF_TU
 hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream, uint64_t n_hint) {
   const uint64_t grid = std::max<uint64_t>(4 * (uint64_t)num_cus, std::min<uint64_t>(n_hint / 1024 + 1, 1u << 16));
   hipLaunchKernelGGL(wheel_offsets_kernel, dim3((uint32_t)grid), dim3(256), 0, stream, table);
@@ -1676,6 +1742,7 @@ hipError_t free_scratch(Scratch* s) {
   s->used = false;
   return e != hipSuccess ? e : f != hipSuccess ? f : g;
 }
+#endif  // !DSE_WHEEL_HALF_TU
 
 namespace {
 
@@ -1717,6 +1784,20 @@ WheelArgs make_wheel_args(uint64_t g_start, uint64_t nbits, uint64_t* plane_lut)
   constexpr uint32_t small[] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61};
   for (uint32_t v : small)
     if (v >= v_start && (v - v_start) / 2 < nbits) wa.fix0 |= 1u << ((v - v_start) / 2);
+  // odd primes up to 61, TA, TB and kWheelMaxPrime (sieved once)
+  static const auto counts = [] {
+    std::array<uint32_t, 4> c{};
+    const uint32_t lim[4] = {kQMax, TA, TB, (uint32_t)kWheelMaxPrime};
+    std::vector<uint8_t> comp(kWheelMaxPrime / 2 + 1, 0);  // comp[i]: 2i + 1 composite
+    for (uint64_t i = 1; (2 * i + 1) * (2 * i + 1) <= kWheelMaxPrime; ++i)
+      if (!comp[i])
+        for (uint64_t j = ((2 * i + 1) * (2 * i + 1)) / 2; j <= kWheelMaxPrime / 2; j += 2 * i + 1) comp[j] = 1;
+    for (uint64_t i = 1; 2 * i + 1 <= kWheelMaxPrime; ++i)
+      if (!comp[i])
+        for (int t = 0; t < 4; ++t) c[t] += 2 * i + 1 <= lim[t];
+    return c;
+  }();
+  for (int t = 0; t < 4; ++t) wa.nthr[t] = counts[t];
   for (int j = 0; j < kNQ; ++j) wa.v0q[j] = (uint8_t)(wa.V0 % kQ[j]);
   for (int g = 0; g < kNG; ++g) wa.v0g[g] = (uint16_t)(wa.V0 % gmod(g));
 #ifdef DSE_PHASE_KNOB
@@ -1734,6 +1815,7 @@ uint64_t isqrt64(uint64_t x) {
   return r;
 }
 
+#if !DSE_WHEEL_HALF_TU
 // Rigorous bound on the bucket entries of a pass spanning `span` integers with
 // primes in (a, b]: each prime has <= 8 span / (30 p) + 8 coprime multiples;
 // sum 1/p <= ln(ln b / ln a) + 1/ln^2 a and pi(b) <= 1.25506 b / ln b.
@@ -1778,6 +1860,8 @@ hipError_t release_scratch(Scratch* sc, hipStream_t stream) {
   return e;
 }
 
+#endif  // !DSE_WHEEL_HALF_TU
+
 hipError_t launch_wheel(const void* table, const WheelArgs& wa, uint32_t* out, unsigned long long* count,
                         int num_cus, hipStream_t stream) {
   const uint64_t nseg = (wa.nbits + kWheelOutBits - 1) / kWheelOutBits;
@@ -1788,6 +1872,22 @@ hipError_t launch_wheel(const void* table, const WheelArgs& wa, uint32_t* out, u
 
 }  // namespace
 
+#if DSE_WHEEL_HALF_TU
+// The half-size geometry (this translation unit: 2^16 periods per segment):
+// the tail of a range whose last round of full segments would leave most
+// CUs idle (launch_sieve_range). Primes <= kWheelMaxPrime only.
+hipError_t launch_wheel_range_half(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
+                                   unsigned long long* count, int num_cus, hipStream_t stream) {
+  if (nbits == 0) return hipSuccess;
+  uint64_t plane_lut;
+  return launch_wheel(table, make_wheel_args(g_start, nbits, &plane_lut), out, count, num_cus, stream);
+}
+#else
+// Time of a half-size segment (dse_wheel_half.hip) relative to a full one,
+// and of a launch relative to a round of full segments
+// (profiles/r03/geometry_ab.txt).
+constexpr double kHalfSegCost = DSE_HALF_SEG_COST, kLaunchCost = DSE_LAUNCH_COST;
+
 hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
                               unsigned long long* count, int num_cus, hipStream_t stream, Scratch* scratch,
                               const SieveOpts* opts) {
@@ -1796,8 +1896,25 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
   const uint64_t root = isqrt64(vmax);
   uint64_t plane_lut;
   if (root <= kWheelMaxPrime) {
-    const WheelArgs wa = make_wheel_args(g_start, nbits, &plane_lut);
-    return launch_wheel(table, wa, out, count, num_cus, stream);
+    // Segments go to the num_cus persistent workgroups in rounds; a last,
+    // partial round of full segments leaves CUs idle for a whole segment
+    // time. Its range goes to the half-size geometry instead when that
+    // finishes sooner: (its segments / num_cus rounds) x kHalfSegCost plus
+    // the second launch.
+    const uint32_t geo = opts ? opts->wheel_geometry : 0;  // 0 auto, 1 full only, 2 half only
+    const uint64_t G = (uint64_t)num_cus, nseg = (nbits + kWheelOutBits - 1) / kWheelOutBits;
+    uint64_t F = geo == 2 ? 0 : geo == 1 ? nseg : (nseg / G) * G;  // segments of the full geometry
+    if (geo == 0 && F < nseg) {
+      const uint64_t nhalf = (nbits - F * kWheelOutBits + kWheelOutBits / 2 - 1) / (kWheelOutBits / 2);
+      if (kHalfSegCost * (double)((nhalf + G - 1) / G) + (F ? kLaunchCost : 0.0) >= 1.0) F = nseg;
+    }
+    if (F >= nseg) return launch_wheel(table, make_wheel_args(g_start, nbits, &plane_lut), out, count, num_cus, stream);
+    hipError_t e;
+    if (F && (e = launch_wheel(table, make_wheel_args(g_start, F * kWheelOutBits, &plane_lut), out, count, num_cus,
+                               stream)) != hipSuccess)
+      return e;
+    return launch_wheel_range_half(table, g_start + F * kWheelOutBits, nbits - F * kWheelOutBits,
+                                   out ? out + F * (kWheelOutBits / 32) : nullptr, count, num_cus, stream);
   }
   if (!scratch) return hipErrorInvalidValue;
   // primes above kWheelMaxPrime: passes of <= kBucketMaxSegs segments, each
@@ -1836,7 +1953,7 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     uint32_t* start = reinterpret_cast<uint32_t*>(sc + o_start);
     uint32_t* ent = reinterpret_cast<uint32_t*>(sc + o_ent);
     uint32_t* tmp = reinterpret_cast<uint32_t*>(sc + o_tmp);
-    hipLaunchKernelGGL(bucket_range_kernel, dim3(1), dim3(1), 0, stream, table, vmax_p, ba.split, range);
+    hipLaunchKernelGGL(bucket_range_kernel, dim3(1), dim3(64), 0, stream, table, vmax_p, ba.split, range);
     hipLaunchKernelGGL(bucket_count_kernel, dim3(kBucketCols), dim3(kBucketThreads), 4 * (uint32_t)ns, stream, table,
                        ba, range, cols);
     hipLaunchKernelGGL(bucket_colscan_kernel, dim3((uint32_t)((ns + 3) / 4)), dim3(256), 0, stream, cols,
@@ -1867,5 +1984,6 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
   }
   return hipSuccess;
 }
+#endif  // DSE_WHEEL_HALF_TU
 
 }  // namespace dse

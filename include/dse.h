@@ -185,6 +185,9 @@ int32_t dse_device_status(dse_ctx *ctx);
  *   "bucket_split_log2" = k in 0..63: bucketed primes <= 2^k take the
  *   one-level fill, larger ones the two-level staged fill; 0 = the default
  *   split (2^25).
+ *   "wheel_geometry" = 0 (default): a range's last partial round of full
+ *   segments is sieved as half-size segments when that is faster; 1: full
+ *   segments only; 2: half-size segments only (covers that kernel in tests).
  *   "bucket_cap_divisor" = d >= 0: divide each pass's bucket entry capacity
  *   by d (> 1), forcing the overflow path (DSE_EINTERNAL); 0 or 1 = default.
  * DSE_EINVAL for an unknown name or a value out of range. */

@@ -424,7 +424,7 @@ def test_debug_option_rejects_unknown(ctx):
     with pytest.raises(_dse.DseError):
         ctx.debug_set_option("no_such_option", 1)
     for name, bad in (("bucket_split_log2", 64), ("bucket_split_log2", -1), ("bucket_pass_segments", -1),
-                      ("bucket_cap_divisor", -1)):
+                      ("bucket_cap_divisor", -1), ("wheel_geometry", 3), ("wheel_geometry", -1)):
         with pytest.raises(_dse.DseError):
             ctx.debug_set_option(name, bad)
 
@@ -505,3 +505,23 @@ def test_init_more_devices_than_visible():
         S.Context(num_gpus=n + 1)
     assert e.value.code == -1
     assert f"asked for {n + 1} GPUs, {n} visible" in str(e.value)
+
+
+@pytest.mark.parametrize("geometry", [1, 2])
+def test_segment_geometries_vs_oracle(oracle, geometry):
+    """The full (2^17 periods) and half-size (2^16, dse_wheel_half.hip)
+    segment geometries alone (test-only option wheel_geometry), on ragged and
+    random ranges, bit-exact against the oracle. The default (0) splits a
+    range's last partial round of full segments into half segments; every
+    chunk test covers that path."""
+    from mail_sieve_e import sieve as S
+    rng = np.random.default_rng(0xC0DE + geometry)
+    ranges = [(0, 1), (0, 65), (5, 7), (31, 1000), (2**20 - 64, 2**20 + 128), (10**6, 3 * 2**20 + 17),
+              (123456789, 2**21 - 1), (49_999_999_000, 999), (0, 300 * 983040 + 12345)]
+    ranges += [(int(rng.integers(0, 5 * 10**10)), int(rng.integers(1, 6 * 2**20))) for _ in range(12)]
+    with S.Context(num_gpus=1) as c:
+        c.debug_set_option("wheel_geometry", geometry)
+        for g0, nb in ranges:
+            m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
+            m, cnt = c.sieve_odd_range(g0, nb)
+            assert cnt == c_ref and np.array_equal(m, m_ref), (geometry, g0, nb)
