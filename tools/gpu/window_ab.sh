@@ -1,10 +1,12 @@
+#!/bin/bash
+# Window [1e18, 1e18+1e10] timing (tools/window_bench.py) for library variants, interleaved:
+#   OUT=gpurun_out/<dir> ROUNDS=2 bash tools/gpu/window_ab.sh prod bu ...
 set -o pipefail
-mkdir -p gpurun_out/w
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 200 --timeout-method thread -k "window or bucket" > gpurun_out/w/test.log 2>&1 || { echo TESTFAIL; tail -30 gpurun_out/w/test.log; exit 1; }
-tail -2 gpurun_out/w/test.log
-for r in 1 2; do
-  timeout -k 10 120 python tools/window_bench.py && DSE_LIB=variants/libdse_onelevel.so timeout -k 10 120 python tools/window_bench.py || exit 1
+OUT=${OUT:-gpurun_out/wab}; mkdir -p $OUT
+for r in $(seq 1 ${ROUNDS:-2}); do
+  for v in "$@"; do
+    L=$([ "$v" = prod ] && echo distributed-sieve-e_amd/mail_sieve_e/libdse.so || echo variants/libdse_$v.so)
+    echo -n "$r $v: " | tee -a $OUT/window_ab.txt
+    DSE_LIB=$L timeout -k 10 120 python tools/window_bench.py 2>&1 | tail -1 | tee -a $OUT/window_ab.txt || exit 1
+  done
 done
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 180 rocprofv3 --kernel-trace --stats -d gpurun_out/w/prof -o run -- python tools/window_bench.py > gpurun_out/w/prof.log 2>&1 || exit 1
-find gpurun_out/w/prof -name "*kernel_stats.csv" | head -1 | xargs cat | cut -d, -f1-5 | head -14
