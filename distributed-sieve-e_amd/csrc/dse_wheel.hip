@@ -78,7 +78,7 @@ static_assert(NE >= 1 && NE <= NW && (DSE_PIPELINE ? NE < NW : NE == NW) && ROWS
 #define DSE_TA 256
 #endif
 #ifndef DSE_L_SETS
-#define DSE_L_SETS 1  // sets of 64 primes per L unit (A/B)
+#define DSE_L_SETS 2  // sets of 64 primes per L unit (A/B)
 #endif
 #ifndef DSE_WHEEL_HALF_TU
 #define DSE_WHEEL_HALF_TU 0  // 1: compiled by dse_wheel_half.hip with 2^16 periods per segment
@@ -87,7 +87,7 @@ static_assert(NE >= 1 && NE <= NW && (DSE_PIPELINE ? NE < NW : NE == NW) && ROWS
 #define DSE_HALF_SEG_COST 0.68
 #endif
 #ifndef DSE_LAUNCH_COST
-#define DSE_LAUNCH_COST 0.5
+#define DSE_LAUNCH_COST 0.1
 #endif
 constexpr uint32_t TA = DSE_TA;             // A/B threshold
 #ifndef DSE_TB
@@ -134,6 +134,24 @@ constexpr uint32_t kQInv30[kNQ] = {inv30_const(7),  inv30_const(11), inv30_const
 #ifndef DSE_INIT_REGS
 #define DSE_INIT_REGS 0
 #endif
+#ifndef DSE_PRIO
+#define DSE_PRIO 0  // 1: s_setprio(wave / 4) over expand + init; 2: for the whole kernel (A/B)
+#endif
+#ifndef DSE_BK_NO_M
+#define DSE_BK_NO_M 0  // 1: bucket walks divide in double precision; m[] only for p <= kWheelMaxPrime (A/B)
+#endif
+#ifndef DSE_BK_UNITS
+#define DSE_BK_UNITS 0  // 1: bucketed hits as units of the mark queue (A/B)
+#endif
+#ifndef DSE_BK_UNIT_BATCHES
+#define DSE_BK_UNIT_BATCHES 4
+#endif
+#ifndef DSE_LUT_GLOBAL
+#define DSE_LUT_GLOBAL 0  // 1: expansion table read from global memory (L1) instead of LDS (A/B)
+#endif
+#ifndef DSE_INIT_GLOBAL
+#define DSE_INIT_GLOBAL 0  // 1: init tables read from global memory (L1) instead of LDS (A/B)
+#endif
 constexpr int kNG = 7;
 constexpr uint32_t kGQ[kNG][3] = {{7, 11, 13}, {17, 19, 1}, {23, 29, 1}, {31, 37, 1},
                                   {41, 43, 1}, {47, 53, 1}, {59, 61, 1}};
@@ -171,6 +189,33 @@ constexpr InitTables make_init_tables() {
   return t;
 }
 __device__ const InitTables g_init_tables = make_init_tables();
+#endif
+
+#if DSE_LUT_GLOBAL
+// The expansion table for each of the 15 values of V0 mod 30 (V0 even): entry
+// v ^ 3 (v >> 5) = the prime odd slots of a period whose plane composite bits
+// are v (as the LDS table the kernel builds per launch).
+struct ExpandLuts {
+  uint32_t w[15 * 256];
+};
+constexpr ExpandLuts make_expand_luts() {
+  ExpandLuts t{};
+  for (uint32_t m = 0; m < 15; ++m) {
+    uint32_t rho[8] = {}, n = 0;
+    for (uint32_t r = 1; r < 30; r += 2) {
+      const uint32_t x = (2 * m + r) % 30;
+      if (x % 3 != 0 && x % 5 != 0) rho[n++] = r;
+    }
+    for (uint32_t v = 0; v < 256; ++v) {
+      uint32_t e = 0;
+      for (uint32_t i = 0; i < 8; ++i)
+        if (!(v & (1u << i))) e |= 1u << ((rho[i] - 1) >> 1);
+      t.w[256 * m + (DSE_LUT_GLOBAL == 2 ? v : v ^ (3u * (v >> 5)))] = e;
+    }
+  }
+  return t;
+}
+__device__ const ExpandLuts g_expand_luts = make_expand_luts();
 #endif
 
 struct WheelArgs {
@@ -557,7 +602,7 @@ __device__ __forceinline__ void load_L(LargeOps& o, const uint32_t* __restrict__
 // kk >= KP) is an OR of 0 at a valid address. asm for the same reason as
 // mark_col.
 #ifndef DSE_PRED_EXEC
-#define DSE_PRED_EXEC 0  // 1: predicated-off marks leave the instruction (exec mask) instead of ORing 0 (A/B)
+#define DSE_PRED_EXEC 1  // 0: predicated-off marks OR 0 instead of leaving the instruction (exec mask) (A/B)
 #endif
 template <bool PRED>
 __device__ __forceinline__ void mark_plane(uint32_t pb4, uint32_t kk) {
@@ -713,13 +758,18 @@ __device__ __attribute__((noinline)) void mark_bucket_hits(const uint32_t* __res
   }
 }
 
+constexpr uint32_t kBkBatchU = 16;                                // loads in flight per lane (bucket unit)
+constexpr uint32_t kBkUnit = 64 * kBkBatchU * DSE_BK_UNIT_BATCHES;  // entries per bucket unit
+
 struct WheelLds {
   uint32_t img[NIMG][IMG_WORDS];   // the segment image(s), at LDS address 0
   uint64_t mid_m[kMidCap];         // Barrett factors of the staged mid primes
   uint32_t mid_p[kMidCap];         // p | (30^{-1} mod p) << 16
   uint32_t lut[256];               // period byte -> 15 odd slots
 #if !DSE_INIT_REGS
+#if !DSE_INIT_GLOBAL
   uint4 itab[kGDW];                // init tables U_G, 4 copies shifted by 0..3 dwords (kGDW / 4 blocks each)
+#endif
 #endif
   uint32_t thr[4];
   uint32_t ctr[2];                 // unit counters (pipelined: one per image)
@@ -797,7 +847,9 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     s_lut[tid ^ (3u * (tid >> 5))] = v;
   }
 #if !DSE_INIT_REGS
+#if !DSE_INIT_GLOBAL
   for (uint32_t idx = tid; idx < 4 * kGDW; idx += NT) reinterpret_cast<uint32_t*>(lds.itab)[idx] = g_init_tables.w[idx];
+#endif
 #endif
   __syncthreads();
   const uint32_t i_mid0 = s_thr[0], i_midB = s_thr[1], i_mid1 = s_thr[2];
@@ -894,7 +946,13 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       for (uint32_t r = 0; r < H; ++r) acc[r] = 0;
 #pragma unroll
       for (int g = 0; g < kNG; ++g) {
+#if DSE_INIT_GLOBAL
+        // from the vector L1 (a 10 KB table every CU reads): the reads leave
+        // the LDS to the expansion running beside them
+        const uint4* bp = reinterpret_cast<const uint4*>(g_init_tables.w) + boff[g] + h / 4;
+#else
         const uint4* bp = lds.itab + boff[g] + h / 4;
+#endif
         uint32_t blk[H + 4];
 #pragma unroll
         for (uint32_t b = 0; b < H / 4 + 1; ++b) {
@@ -928,6 +986,9 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     const uint32_t ro = 2 * (2 * (lane >> 5) + gsub) + (k & 1), c = k >> 1;
     const bool odd = k & 1;
     const uint64_t seg_word0 = s * (uint64_t)kOutWordsPerSeg;
+#if DSE_LUT_GLOBAL
+    const uint32_t* __restrict__ g_lut = g_expand_luts.w + 256 * (uint32_t)((wa.V0 % 30) / 2);
+#endif
 #pragma unroll 1
     for (uint32_t t = 0; t < ROWS / (NE * 8); ++t) {
       const uint32_t row = 8 * ((ROWS / (NE * 8)) * wave + t) + ro;
@@ -941,11 +1002,13 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       // LUT index of every period byte v: v ^ 3 (v >> 5), a bijection that
       // puts the common bytes (all composite, one prime) in distinct banks
       // (indexed by v, 255 / 223 / 191 / 127 would share bank 31)
+#if DSE_LUT_GLOBAL != 2  // (2: the global table is indexed by v itself: no banks to spread)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint32_t h = (W[j] >> 5) & 0x07070707u;
         W[j] ^= h + (h << 1);  // 3h <= 21: no carry into the next byte
       }
+#endif
       uint32_t o[15];
 #pragma unroll
       for (int w = 0; w < 15; ++w) o[w] = 0;
@@ -953,7 +1016,11 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       for (int q = 0; q < 4; ++q) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
+#if DSE_LUT_GLOBAL
+          const uint32_t e = g_lut[(W[j] >> (8 * q)) & 0xFFu];  // vector L1: no LDS bank conflicts
+#else
           const uint32_t e = s_lut[(W[j] >> (8 * q)) & 0xFFu];
+#endif
           const int pos = 15 * (8 * q + j);
           o[pos >> 5] |= e << (pos & 31);
           if ((pos & 31) > 17) o[(pos >> 5) + 1] |= e >> (32 - (pos & 31));
@@ -1001,9 +1068,21 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     const uint32_t img0 = lds_addr(img);
     // bucketed hits of the primes > kWheelMaxPrime: one entry per marking
     // thread (pipelined: the non-expander waves)
+#if DSE_BK_UNITS
+    // bucketed hits as units of the queue (kBkUnit entries each), interleaved
+    // with the marking units, so their global-load latency overlaps other
+    // waves' marking instead of stalling every wave at the segment start
+    uint32_t bk_b0 = 0, n3 = 0;
+    if (wa.bk_start && (phases & kPhaseLarge)) {
+      bk_b0 = wa.bk_start[s];
+      n3 = (wa.bk_start[s + 1] - bk_b0 + kBkUnit - 1) / kBkUnit;
+    }
+    const uint32_t bk_b1 = n3 ? wa.bk_start[s + 1] : 0u;
+#else
     constexpr uint32_t kMarkT0 = DSE_PIPELINE ? NE * 64 : 0;
     if (wa.bk_start && (phases & kPhaseLarge) && tid >= kMarkT0)
       mark_bucket_hits(wa.bk_entries, wa.bk_start[s], wa.bk_start[s + 1], tid - kMarkT0, NT - kMarkT0, img0);
+#endif
     const uint32_t rot = (i_mid1 + lane) & 7;  // = table index & 7 of this lane's large primes
     // absolute residue (q + rot) & 7 at step q: its plane and e bit
     const uint32_t pl_rot = ((wa.pl_pack >> (3 * rot)) | (wa.pl_pack << (24 - 3 * rot))) & 0xFFFFFFu;
@@ -1037,26 +1116,58 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     };
     auto is_l = [&](uint32_t u) -> bool { return u < 2 * n_int ? (u & 1) != 0 : n2 > n1; };
     auto idx_of = [&](uint32_t u) -> uint32_t { return u < 2 * n_int ? u >> 1 : u - n_int; };
+#if DSE_BK_UNITS
+    // queue position -> marking unit (or ~0u: bucket unit bk_of(q)); the n3
+    // bucket units interleave 1:1 with the marking units from the start
+    const uint32_t mb = min(n3, n_all), n_q = n_all + n3;
+    auto unit_of = [&](uint32_t q) -> uint32_t {
+      if (q < 2 * mb) return (q & 1) ? ~0u : q >> 1;
+      return n3 > n_all ? ~0u : q - mb;
+    };
+    auto bk_of = [&](uint32_t q) -> uint32_t { return q < 2 * mb ? q >> 1 : q - mb; };
+#else
+    const uint32_t n_q = n_all;
+    auto unit_of = [&](uint32_t q) -> uint32_t { return q; };
+#endif
     LargeOps cur, nxt;
 #if DSE_L_SETS == 2
     LargeOps cur1, nxt1;  // the unit's second 64 primes
 #endif
-    uint32_t u_cur = claimed(claim());
-    uint32_t u_nxt = claimed(claim());
-    if (u_cur < n_all && is_l(u_cur)) {
-      load_L(cur, P, M, A, i_mid1 + kLU * idx_of(u_cur) + lane, i_big);
+    uint32_t q_cur = claimed(claim());
+    uint32_t q_nxt = claimed(claim());
+    if (q_cur < n_q && unit_of(q_cur) != ~0u && is_l(unit_of(q_cur))) {
+      load_L(cur, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_cur)) + lane, i_big);
 #if DSE_L_SETS == 2
-      load_L(cur1, P, M, A, i_mid1 + kLU * idx_of(u_cur) + 64 + lane, i_big);
+      load_L(cur1, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_cur)) + 64 + lane, i_big);
 #endif
     }
-    while (u_cur < n_all) {
+    while (q_cur < n_q) {
       const uint32_t c2 = claim();  // unit after next, read at the end of this one
-      if (u_nxt < n_all && is_l(u_nxt)) {
-        load_L(nxt, P, M, A, i_mid1 + kLU * idx_of(u_nxt) + lane, i_big);
+      if (q_nxt < n_q && unit_of(q_nxt) != ~0u && is_l(unit_of(q_nxt))) {
+        load_L(nxt, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_nxt)) + lane, i_big);
 #if DSE_L_SETS == 2
-        load_L(nxt1, P, M, A, i_mid1 + kLU * idx_of(u_nxt) + 64 + lane, i_big);
+        load_L(nxt1, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_nxt)) + 64 + lane, i_big);
 #endif
       }
+      const uint32_t u_cur = unit_of(q_cur);
+#if DSE_BK_UNITS
+      if (u_cur == ~0u) {  // a bucket unit: kBkUnit entries, kBkBatch loads in flight per lane
+        const uint32_t beg = bk_b0 + bk_of(q_cur) * kBkUnit, end = min(bk_b1, beg + kBkUnit);
+        for (uint32_t j = beg + lane; j < end; j += 64 * kBkBatchU) {
+          uint32_t e[kBkBatchU];
+#pragma unroll
+          for (uint32_t t = 0; t < kBkBatchU; ++t)
+            e[t] = j + 64 * t < end ? __builtin_nontemporal_load(wa.bk_entries + j + 64 * t) : 0u;
+#pragma unroll
+          for (uint32_t t = 0; t < kBkBatchU; ++t)
+            if (j + 64 * t < end) mark_plane<false>(img0 + 4 * (e[t] >> kWheelLogKP), e[t] & (KP - 1));
+        }
+        cur = nxt;
+        q_cur = q_nxt;
+        q_nxt = claimed(c2);
+        continue;
+      }
+#endif
       const uint32_t k = idx_of(u_cur);
 #ifdef DSE_TIMING
       const uint64_t t_u0 = __builtin_amdgcn_s_memtime();
@@ -1091,8 +1202,8 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
 #if DSE_L_SETS == 2
       cur1 = nxt1;
 #endif
-      u_cur = u_nxt;
-      u_nxt = claimed(c2);
+      q_cur = q_nxt;
+      q_nxt = claimed(c2);
     }
   };
 
@@ -1116,6 +1227,18 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     }
   }
 #else
+#if DSE_PRIO
+  const uint32_t wave_u = __builtin_amdgcn_readfirstlane(wave);
+  auto set_prio = [](uint32_t pr) {  // s_setprio takes an immediate
+    if (pr == 0) __builtin_amdgcn_s_setprio(0);
+    else if (pr == 1) __builtin_amdgcn_s_setprio(1);
+    else if (pr == 2) __builtin_amdgcn_s_setprio(2);
+    else __builtin_amdgcn_s_setprio(3);
+  };
+#if DSE_PRIO == 2
+  set_prio(wave_u >> 2);
+#endif
+#endif
   if (T > 0) init_segment(lds.img[0], blockIdx.x);
   __syncthreads();
   DSE_TSTAMP(0);
@@ -1126,12 +1249,18 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     DSE_TSTAMP(1);
     __syncthreads();
     DSE_TSTAMP(2);
+#if DSE_PRIO == 1
+    set_prio(wave_u >> 2);  // the statically split phase: younger waves (a SIMD's later ones) first
+#endif
     if (phases & kPhaseExpand) expand_segment(lds.img[0], s);
     DSE_TSTAMP(3);
     // init of this workgroup's next segment, on the rows this wave just
     // expanded: no barrier in between, and waves drift into init while
     // others still expand
     if (t + 1 < T) init_segment(lds.img[0], s + grid);
+#if DSE_PRIO == 1
+    __builtin_amdgcn_s_setprio(0);
+#endif
     if (tid == 0) lds.ctr[0] = 0;  // all claims of this segment returned before the barrier above
     DSE_TSTAMP(4);
     __syncthreads();
@@ -1180,9 +1309,15 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
   uint32_t* A = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + table_a_offset(h->cap));
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t p = P[i];
+#if DSE_BK_NO_M
+    if (p > kWheelMaxPrime) continue;  // bucketed primes: the walks divide in double precision
+    const uint64_t m = barrett_factor(p);
+    M[i] = m;
+#else
     const uint64_t m = barrett_factor(p);
     M[i] = m;
     if (p > kWheelMaxPrime) continue;  // bucketed primes: the walk needs m only, never the rows
+#endif
     if (p < 7) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) A[8ull * i + j] = 0;
@@ -1283,9 +1418,20 @@ __global__ __launch_bounds__(64) void bucket_range_kernel(const void* __restrict
 __device__ __forceinline__ uint64_t bucket_first(uint32_t p, uint64_t m, const BucketArgs& ba, uint32_t& w3) {
   const uint64_t p2 = (uint64_t)p * p;
   const uint64_t vlo = max(ba.V0 + 1, p2);
+#if DSE_BK_NO_M
+  // floor(vlo / p) from a double quotient: vlo < 2^62 rounds by < 2^9 and
+  // p > 2^20, so the estimate is within 1 of the truth; corrected exactly
+  (void)m;
+  uint64_t q = (uint64_t)((double)vlo / (double)p);
+  int64_t rs = (int64_t)(vlo - q * p);
+  while (rs < 0) { rs += p; --q; }
+  while (rs >= (int64_t)p) { rs -= p; ++q; }
+  uint64_t r = (uint64_t)rs;
+#else
   uint64_t q = __umul64hi(vlo, m);  // floor(vlo / p), corrected
   uint64_t r = vlo - q * p;
   while (r >= p) { r -= p; ++q; }
+#endif
   const uint64_t m0 = q + (r != 0);
   const uint32_t r30 = (uint32_t)(m0 % 30);
   const uint32_t d = __builtin_ctz(kCoprime30 >> r30);
@@ -1322,7 +1468,7 @@ __device__ __forceinline__ void for_bucket_primes(const uint32_t* __restrict__ P
   uint32_t base = i_lo, i = i_lo + j;
   if (i >= i_hi) return;
   uint32_t pn = P[i];
-  uint64_t mn = M[i];
+  uint64_t mn = DSE_BK_NO_M ? 0 : M[i];
   for (bool odd = false;;) {  // round indices increase, so the first one past i_hi ends the walk
     const uint32_t p = pn;
     const uint64_t m = mn;
@@ -1332,7 +1478,7 @@ __device__ __forceinline__ void for_bucket_primes(const uint32_t* __restrict__ P
     const bool more = i < i_hi;
     if (more) {
       pn = P[i];
-      mn = M[i];
+      mn = DSE_BK_NO_M ? 0 : M[i];
     }
     walk(p, m);
     if (!more) break;
@@ -1541,7 +1687,7 @@ __device__ __forceinline__ void bucket_stage_wg(uint32_t* sm, uint32_t b, const 
   uint64_t mn = 0;
   if (i < i_hi) {
     pn = P[i];
-    mn = M[i];
+    mn = DSE_BK_NO_M ? 0 : M[i];
   }
   uint32_t p = 0, w3 = 0;
   uint64_t o = ba.span;
@@ -1553,7 +1699,7 @@ __device__ __forceinline__ void bucket_stage_wg(uint32_t* sm, uint32_t b, const 
       i += stride;
       if (i < i_hi) {
         pn = P[i];
-        mn = M[i];
+        mn = DSE_BK_NO_M ? 0 : M[i];
       }
       o = bucket_first(p, m, ba, w3);
       if (o < ba.span) return;
