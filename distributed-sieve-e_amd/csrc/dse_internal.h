@@ -9,7 +9,8 @@ namespace dse {
 // Base-prime table: one flat device buffer so ranks can broadcast it as bytes.
 //   [0,16)            header {count, cap, limit}
 //   [16, 16+4cap)     uint32 p[cap]      odd primes <= limit, ascending
-//   [align8(...), +8cap) uint64 m[cap]  Barrett factors floor((2^64-1)/p)
+//   [align8(...), +8cap) uint64 m[cap]  Barrett factors floor((2^64-1)/p) of the primes <= kWheelMaxPrime
+//                                        (the bucketed primes' walks divide in double precision)
 //   [align32(..), +32cap) uint32 a[8cap] wheel offsets, row i rotated by i mod 8:
 //                                        a[8i+j] = first k >= 0 with p | R30[(j+i)&7] + 30k
 //                                        (p >= 7; 0 for p = 3, 5)

@@ -138,10 +138,10 @@ constexpr uint32_t kQInv30[kNQ] = {inv30_const(7),  inv30_const(11), inv30_const
 #define DSE_PRIO 0  // 1: s_setprio(wave / 4) over expand + init; 2: for the whole kernel (A/B)
 #endif
 #ifndef DSE_BK_NO_M
-#define DSE_BK_NO_M 0  // 1: bucket walks divide in double precision; m[] only for p <= kWheelMaxPrime (A/B)
+#define DSE_BK_NO_M 1  // 0: bucket walks read m[] (Barrett factors of every table prime) (A/B)
 #endif
 #ifndef DSE_BK_UNITS
-#define DSE_BK_UNITS 0  // 1: bucketed hits as units of the mark queue (A/B)
+#define DSE_BK_UNITS 1  // 0: bucketed hits marked by every wave before the units (A/B)
 #endif
 #ifndef DSE_BK_UNIT_BATCHES
 #define DSE_BK_UNIT_BATCHES 4
@@ -1163,6 +1163,9 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
             if (j + 64 * t < end) mark_plane<false>(img0 + 4 * (e[t] >> kWheelLogKP), e[t] & (KP - 1));
         }
         cur = nxt;
+#if DSE_L_SETS == 2
+        cur1 = nxt1;
+#endif
         q_cur = q_nxt;
         q_nxt = claimed(c2);
         continue;

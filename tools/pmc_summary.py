@@ -17,11 +17,18 @@ NUM_CUS = 256
 
 
 def load(root, pat):
-    v = collections.defaultdict(lambda: collections.defaultdict(float))
+    """Dispatches of the largest grid only (a range's tail may be a second,
+    half-geometry launch of the same kernel name)."""
+    rows = []
     for f in glob.glob(os.path.join(root, "pmc_*.csv")):
-        for r in csv.DictReader(open(f)):
-            if pat in r["Kernel_Name"]:
-                v[r["Counter_Name"]][(os.path.basename(f), r["Dispatch_Id"])] += float(r["Counter_Value"])
+        rows += [(os.path.basename(f), r) for r in csv.DictReader(open(f)) if pat in r["Kernel_Name"]]
+    if not rows:
+        return {}
+    grid = max(int(r["Grid_Size"]) for _, r in rows)
+    v = collections.defaultdict(lambda: collections.defaultdict(float))
+    for f, r in rows:
+        if int(r["Grid_Size"]) == grid:
+            v[r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
     return {k: sum(d.values()) / len(d) for k, d in v.items()}
 
 
