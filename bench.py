@@ -118,7 +118,10 @@ def pmc_summary(N: int, P: int, window: bool):
     gfx950 FETCH_SIZE counts half of a wide coalesced read, WRITE_SIZE is exact);
     VALU issue against the 2.0 wave-instructions per CU-cycle ceiling, LDS busy
     (SQ_LDS_IDX_ACTIVE per CU-cycle) and the bank-conflict share of it
-    (GRBM_GUI_ACTIVE is summed over the 8 XCDs)."""
+    (GRBM_GUI_ACTIVE is summed over the 8 XCDs). Figures are per step: a
+    step's range may run as a main launch plus a half-geometry tail launch
+    (DESIGN.md section 4.1.2), so each counter is summed over every row of
+    the kernel and divided by the number of main (largest-grid) dispatches."""
     import collections
     import csv
     import glob
@@ -126,13 +129,18 @@ def pmc_summary(N: int, P: int, window: bool):
         return None
     for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")), reverse=True):
         try:
-            vals = collections.defaultdict(list)
+            tot = collections.defaultdict(float)
+            steps = {}
             for f in ("pmc_fetch_sieve_kernel.csv", "pmc_write_sieve_kernel.csv", "pmc_sq_sieve_kernel.csv",
                       "pmc_wait_sieve_kernel.csv"):
-                for r in csv.DictReader(open(os.path.join(d, f))):
-                    if "wheel_segments_kernel" in r["Kernel_Name"]:
-                        vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-            v = {k: sum(x) / len(x) for k, x in vals.items()}
+                rows = [r for r in csv.DictReader(open(os.path.join(d, f)))
+                        if "wheel_segments_kernel" in r["Kernel_Name"]]
+                grid = max(int(r["Grid_Size"]) for r in rows)
+                for r in rows:
+                    tot[r["Counter_Name"]] += float(r["Counter_Value"])
+                    if int(r["Grid_Size"]) == grid:
+                        steps.setdefault(r["Counter_Name"], set()).add(r["Dispatch_Id"])
+            v = {k: x / len(steps[k]) for k, x in tot.items()}
             cyc = v["GRBM_GUI_ACTIVE"] / 8
             return {"traffic": (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024, "source": os.path.relpath(d, ROOT),
                     "cycles": cyc,

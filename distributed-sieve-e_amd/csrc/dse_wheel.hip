@@ -248,16 +248,25 @@ __device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
 // offset (off >> 5) * 256 (< 64 KiB) and the column combine with one v_and_or.
 // Issued as asm: callers drain lgkmcnt before a barrier (lds_drain), since the
 // compiler's waitcnt pass does not see it.
-__device__ __forceinline__ void mark_col(uint32_t cb, uint32_t off) {
+__device__ __forceinline__ void mark_col(uint32_t cb, uint32_t off, uint32_t one) {
   uint32_t a, b;
   asm volatile(
       "v_lshlrev_b32 %0, 3, %2\n\t"
       "v_and_or_b32 %0, %0, %4, %3\n\t"
-      "v_lshlrev_b32 %1, %2, 1\n\t"
+      "v_lshlrev_b32 %1, %2, %5\n\t"
       "ds_or_b32 %0, %1"
       : "=&v"(a), "=&v"(b)
-      : "v"(off), "v"(cb), "s"(0xffffff00u)
+      : "v"(off), "v"(cb), "s"(0xffffff00u), "v"(one)
       : "memory");
+}
+
+// 1 << (x & 31) as a 4-byte VOP2 (the shifted 1 in a VGPR: with the inline
+// constant in the value operand the instruction needs the 8-byte VOP3 form,
+// and the wheel kernel is bound by instruction fetch)
+__device__ __forceinline__ uint32_t shl1(uint32_t x, uint32_t one) {
+  uint32_t r;
+  asm("v_lshlrev_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(one));
+  return r;
 }
 
 __device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -272,39 +281,39 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x) {
 // Mark period `off` of the column at cb and advance off by p, in one asm
 // block (written as mark_col + an add, the loop-carried offset costs a
 // v_mov per mark).
-__device__ __forceinline__ void mark_col_step(uint32_t cb, uint32_t& off, uint32_t p) {
+__device__ __forceinline__ void mark_col_step(uint32_t cb, uint32_t& off, uint32_t p, uint32_t one) {
   uint32_t a, b;
   asm volatile(
       "v_lshlrev_b32 %0, 3, %2\n\t"
       "v_and_or_b32 %0, %0, %4, %3\n\t"
-      "v_lshlrev_b32 %1, %2, 1\n\t"
+      "v_lshlrev_b32 %1, %2, %6\n\t"
       "ds_or_b32 %0, %1\n\t"
       "v_add_u32 %2, %2, %5"
       : "=&v"(a), "=&v"(b), "+v"(off)
-      : "v"(cb), "s"(0xffffff00u), "v"(p)
+      : "v"(cb), "s"(0xffffff00u), "v"(p), "v"(one)
       : "memory");
 }
 
 // n unconditional marks off, off + p, ... in one column, unrolled by 4 by
 // hand (the asm marks keep the compiler from unrolling, which costs three
 // SALU of loop control per mark); returns the offset after the run.
-__device__ __forceinline__ uint32_t mark_run(uint32_t cb, uint32_t off, uint32_t p, uint32_t n) {
+__device__ __forceinline__ uint32_t mark_run(uint32_t cb, uint32_t off, uint32_t p, uint32_t n, uint32_t one) {
   uint32_t h = 0;
   for (; h + 4 <= n; h += 4) {
-    mark_col_step(cb, off, p);
-    mark_col_step(cb, off, p);
-    mark_col_step(cb, off, p);
-    mark_col_step(cb, off, p);
+    mark_col_step(cb, off, p, one);
+    mark_col_step(cb, off, p, one);
+    mark_col_step(cb, off, p, one);
+    mark_col_step(cb, off, p, one);
   }
-  for (; h < n; ++h) mark_col_step(cb, off, p);
+  for (; h < n; ++h) mark_col_step(cb, off, p, one);
   return off;
 }
 
 // Mark period `off` of the column at byte address cb if off < LS (else an OR
 // of 0 at a row inside the column); returns the offset of the next hit.
-__device__ __forceinline__ uint32_t mark_col_pred(uint32_t cb, uint32_t off, uint32_t p) {
+__device__ __forceinline__ uint32_t mark_col_pred(uint32_t cb, uint32_t off, uint32_t p, uint32_t one) {
   const bool hit = off < LS;
-  const uint32_t bit = hit ? 1u << (off & 31) : 0u;
+  const uint32_t bit = hit ? shl1(off, one) : 0u;
   uint32_t a;
   asm volatile(
       "v_lshlrev_b32 %0, 3, %1\n\t"
@@ -406,15 +415,15 @@ __device__ __forceinline__ uint32_t kmin_for(uint32_t D, uint32_t rho) {
 // pb = LDS byte address of the plane's word in column 0 (image + 4 * plane).
 template <int NX>
 __device__ __forceinline__ void diag_walk(uint32_t off, uint32_t p, uint32_t pb, uint32_t c, uint32_t O0,
-                                          uint32_t n_u, uint32_t n_x) {
+                                          uint32_t n_u, uint32_t n_x, uint32_t one) {
   for (uint32_t t = 0; t < 8; ++t) {
     const uint32_t cb_col = pb + 32 * c;
-    off = mark_run(cb_col, off, p, n_u);
+    off = mark_run(cb_col, off, p, n_u, one);
     if (NX >= 0) {
 #pragma unroll
-      for (int h = 0; h < NX; ++h) off = mark_col_pred(cb_col, off, p);
+      for (int h = 0; h < NX; ++h) off = mark_col_pred(cb_col, off, p, one);
     } else {
-      for (uint32_t h = 0; h < n_x; ++h) off = mark_col_pred(cb_col, off, p);
+      for (uint32_t h = 0; h < n_x; ++h) off = mark_col_pred(cb_col, off, p, one);
     }
     off -= LS;
     c = (c + 1) & 7;
@@ -473,7 +482,7 @@ constexpr uint32_t TA_CLS = DSE_TA_CLS;
 constexpr uint32_t IMG_BYTES = IMG_WORDS * 4;
 static_assert((IMG_BYTES & (IMG_BYTES - 1)) == 0, "image size is a power of two");
 template <int K>
-__device__ __forceinline__ void a_classes(uint32_t img0, uint32_t cb_col, uint32_t off, uint32_t p) {
+__device__ __forceinline__ void a_classes(uint32_t img0, uint32_t cb_col, uint32_t off, uint32_t p, uint32_t one) {
   const uint32_t D = p << 8;  // p rows
 #pragma unroll 1
   for (uint32_t n0 = 0; n0 < 32; ++n0) {
@@ -481,9 +490,9 @@ __device__ __forceinline__ void a_classes(uint32_t img0, uint32_t cb_col, uint32
     asm volatile(
         "v_lshlrev_b32 %0, 3, %2\n\t"
         "v_and_or_b32 %0, %0, %3, %4\n\t"
-        "v_lshlrev_b32 %1, %2, 1"
+        "v_lshlrev_b32 %1, %2, %5"
         : "=&v"(a), "=&v"(bit)
-        : "v"(off), "s"(0xffffff00u), "v"(cb_col));
+        : "v"(off), "s"(0xffffff00u), "v"(cb_col), "v"(one));
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       mark_at(a, bit);
@@ -498,7 +507,7 @@ __device__ __forceinline__ void a_classes(uint32_t img0, uint32_t cb_col, uint32
 // A: one mid prime (61 < p <= TA) per wave; lane L walks column L =
 // (plane L&7, column L>>3).
 __device__ __forceinline__ void unit_A(uint32_t* __restrict__ img, uint32_t pi, uint64_t m, uint64_t Vs,
-                                       uint64_t rho_pack, uint32_t lane) {
+                                       uint64_t rho_pack, uint32_t lane, uint32_t one) {
   const uint32_t p = pi & 0xFFFFu, inv30 = pi >> 16;  // wave-uniform
   const uint64_t p2 = (uint64_t)p * p;
   const uint32_t Xs = mod_barrett(Vs, p, m);            // scalar unit
@@ -513,22 +522,22 @@ __device__ __forceinline__ void unit_A(uint32_t* __restrict__ img, uint32_t pi, 
     const uint32_t K = ROWS / p;  // wave-uniform, scalar
     if (p < TA_CLS) {
       switch (K) {  // ROWS / p for 61 < p < TA_CLS
-        case 2: a_classes<2>(lds_addr(img), cb_col, off, p); return;
-        case 3: a_classes<3>(lds_addr(img), cb_col, off, p); return;
-        case 4: a_classes<4>(lds_addr(img), cb_col, off, p); return;
-        case 5: a_classes<5>(lds_addr(img), cb_col, off, p); return;
-        case 6: a_classes<6>(lds_addr(img), cb_col, off, p); return;
-        case 7: a_classes<7>(lds_addr(img), cb_col, off, p); return;
+        case 2: a_classes<2>(lds_addr(img), cb_col, off, p, one); return;
+        case 3: a_classes<3>(lds_addr(img), cb_col, off, p, one); return;
+        case 4: a_classes<4>(lds_addr(img), cb_col, off, p, one); return;
+        case 5: a_classes<5>(lds_addr(img), cb_col, off, p, one); return;
+        case 6: a_classes<6>(lds_addr(img), cb_col, off, p, one); return;
+        case 7: a_classes<7>(lds_addr(img), cb_col, off, p, one); return;
         default: break;
       }
     }
     const uint32_t n_full = div_small(LS, p, invp);
-    off = mark_run(cb_col, off, p, n_full);
-    if (off < LS) mark_col(cb_col, off);
+    off = mark_run(cb_col, off, p, n_full, one);
+    if (off < LS) mark_col(cb_col, off, one);
   } else {
     const uint32_t kmin = kmin_for((uint32_t)(p2 - Vs), rho);
     const uint32_t kf = first_at_or_after(kp, max(kmin, c * LS), p, invp);
-    for (uint32_t off = kf - c * LS; off < LS; off += p) mark_col(cb_col, off);
+    for (uint32_t off = kf - c * LS; off < LS; off += p) mark_col(cb_col, off, one);
   }
 }
 
@@ -538,7 +547,7 @@ __device__ __forceinline__ void unit_A(uint32_t* __restrict__ img, uint32_t pi, 
 // 8 planes: 32 distinct banks 8 (c mod 4) + pl.
 __device__ __forceinline__ void unit_B(uint32_t* __restrict__ img, const uint32_t* __restrict__ s_mid_p,
                                        const uint64_t* __restrict__ s_mid_m, uint32_t j0, uint32_t nj, uint64_t Vs,
-                                       uint64_t Vend, uint64_t rho_pack, uint32_t lane) {
+                                       uint64_t Vend, uint64_t rho_pack, uint32_t lane, uint32_t one) {
   const uint32_t pfirst = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
   const uint32_t pl = lane & 7, jp = lane >> 3;
   const bool valid = jp < nj;
@@ -571,9 +580,9 @@ __device__ __forceinline__ void unit_B(uint32_t* __restrict__ img, const uint32_
   // lanes past the batch end mark nothing (their unconditional marks would
   // land in another prime's columns)
   if (!valid) return;
-  if (n_x == 1) diag_walk<1>(off, p, pb, jp, O0, n_u, 1);
-  else if (n_x == 2) diag_walk<2>(off, p, pb, jp, O0, n_u, 2);
-  else diag_walk<-1>(off, p, pb, jp, O0, n_u, n_x);
+  if (n_x == 1) diag_walk<1>(off, p, pb, jp, O0, n_u, 1, one);
+  else if (n_x == 2) diag_walk<2>(off, p, pb, jp, O0, n_u, 2, one);
+  else diag_walk<-1>(off, p, pb, jp, O0, n_u, n_x, one);
 }
 
 // Operands of one large unit, loaded ahead of use. The table row of prime i
@@ -605,7 +614,7 @@ __device__ __forceinline__ void load_L(LargeOps& o, const uint32_t* __restrict__
 #define DSE_PRED_EXEC 1  // 0: predicated-off marks OR 0 instead of leaving the instruction (exec mask) (A/B)
 #endif
 template <bool PRED>
-__device__ __forceinline__ void mark_plane(uint32_t pb4, uint32_t kk) {
+__device__ __forceinline__ void mark_plane(uint32_t pb4, uint32_t kk, uint32_t one) {
 #if DSE_PRED_EXEC
   // a lane without a hit takes no part in the ds_or, so it adds no bank
   // conflict (an OR of 0 at a random column conflicts like a mark)
@@ -614,8 +623,10 @@ __device__ __forceinline__ void mark_plane(uint32_t pb4, uint32_t kk) {
 #else
   constexpr bool kOr0 = PRED;
 #endif
-  const uint32_t col = __builtin_amdgcn_ubfe(kk, LOG_LS, 3);
-  uint32_t bit = 1u << (kk & 31);
+  // kk < KP wherever the mark is executed: the column is kk >> LOG_LS (a
+  // 4-byte shift, not an 8-byte bfe)
+  const uint32_t col = kOr0 ? __builtin_amdgcn_ubfe(kk, LOG_LS, 3) : kk >> LOG_LS;
+  uint32_t bit = shl1(kk, one);
   if (kOr0) bit = kk < KP ? bit : 0u;
   uint32_t a, t;
   asm volatile(
@@ -638,6 +649,7 @@ __device__ __forceinline__ void mark_plane(uint32_t pb4, uint32_t kk) {
 struct PlaneSteps {
   uint32_t pb[8];
   uint32_t ne[8];
+  uint32_t one;  // 1 in a VGPR (shl1)
 };
 
 // Branch-free body of an L unit whose 64 primes are all live and past p^2
@@ -654,22 +666,22 @@ __device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, co
     uint32_t kk = min(t, t + p);  // plane start (a - Kb - e) mod p
     const uint32_t pb4 = ps.pb[q];
     if (MODE == 2) {
-      mark_plane<true>(pb4, kk);
+      mark_plane<true>(pb4, kk, ps.one);
     } else if (MODE == 1) {
-      mark_plane<true>(pb4, kk);
-      mark_plane<true>(pb4, kk + p);
+      mark_plane<true>(pb4, kk, ps.one);
+      mark_plane<true>(pb4, kk + p, ps.one);
     } else {
       uint32_t h = 0;
       for (; h + 2 <= n_min; h += 2) {  // unrolled by hand (asm marks)
-        mark_plane<false>(pb4, kk);
-        mark_plane<false>(pb4, opaque(kk + p));
+        mark_plane<false>(pb4, kk, ps.one);
+        mark_plane<false>(pb4, opaque(kk + p), ps.one);
         kk = opaque(kk + 2 * p);
       }
       if (h < n_min) {
-        mark_plane<false>(pb4, kk);
+        mark_plane<false>(pb4, kk, ps.one);
         kk = opaque(kk + p);
       }
-      for (; kk < KP; kk += p) mark_plane<false>(pb4, kk);  // a predicated fixed-count tail is slower
+      for (; kk < KP; kk += p) mark_plane<false>(pb4, kk, ps.one);  // a predicated fixed-count tail is slower
     }
   }
 }
@@ -728,10 +740,10 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
     }
     const uint32_t pb4 = ps.pb[q];
     if (pmin > KP / 2) {
-      mark_plane<true>(pb4, kk);
-      mark_plane<true>(pb4, kk + p);
+      mark_plane<true>(pb4, kk, ps.one);
+      mark_plane<true>(pb4, kk + p, ps.one);
     } else {
-      for (; kk < KP; kk += p) mark_plane<false>(pb4, kk);
+      for (; kk < KP; kk += p) mark_plane<false>(pb4, kk, ps.one);
     }
   }
 }
@@ -742,7 +754,7 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
 // kernel spent most of its time here). Not inlined: its registers stay out
 // of the unit loop's allocation.
 __device__ __attribute__((noinline)) void mark_bucket_hits(const uint32_t* __restrict__ ent, uint32_t b0, uint32_t b1,
-                                                         uint32_t t, uint32_t T, uint32_t img0) {
+                                                         uint32_t t, uint32_t T, uint32_t img0, uint32_t one) {
   constexpr uint32_t kBkBatch = 16;
   uint32_t j = b0 + t;
   for (; j + (kBkBatch - 1) * T < b1; j += kBkBatch * T) {
@@ -750,11 +762,11 @@ __device__ __attribute__((noinline)) void mark_bucket_hits(const uint32_t* __res
 #pragma unroll
     for (uint32_t q = 0; q < kBkBatch; ++q) e[q] = __builtin_nontemporal_load(ent + j + q * T);
 #pragma unroll
-    for (uint32_t q = 0; q < kBkBatch; ++q) mark_plane<false>(img0 + 4 * (e[q] >> kWheelLogKP), e[q] & (KP - 1));
+    for (uint32_t q = 0; q < kBkBatch; ++q) mark_plane<false>(img0 + 4 * (e[q] >> kWheelLogKP), e[q] & (KP - 1), one);
   }
   for (; j < b1; j += T) {
     const uint32_t e = ent[j];
-    mark_plane<false>(img0 + 4 * (e >> kWheelLogKP), e & (KP - 1));
+    mark_plane<false>(img0 + 4 * (e >> kWheelLogKP), e & (KP - 1), one);
   }
 }
 
@@ -1066,6 +1078,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     uint32_t lane = lane_id;
     asm volatile("" : "+v"(lane));
     const uint32_t img0 = lds_addr(img);
+    const uint32_t one = opaque(1u);
     // bucketed hits of the primes > kWheelMaxPrime: one entry per marking
     // thread (pipelined: the non-expander waves)
 #if DSE_BK_UNITS
@@ -1081,13 +1094,14 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
 #else
     constexpr uint32_t kMarkT0 = DSE_PIPELINE ? NE * 64 : 0;
     if (wa.bk_start && (phases & kPhaseLarge) && tid >= kMarkT0)
-      mark_bucket_hits(wa.bk_entries, wa.bk_start[s], wa.bk_start[s + 1], tid - kMarkT0, NT - kMarkT0, img0);
+      mark_bucket_hits(wa.bk_entries, wa.bk_start[s], wa.bk_start[s + 1], tid - kMarkT0, NT - kMarkT0, img0, one);
 #endif
     const uint32_t rot = (i_mid1 + lane) & 7;  // = table index & 7 of this lane's large primes
     // absolute residue (q + rot) & 7 at step q: its plane and e bit
     const uint32_t pl_rot = ((wa.pl_pack >> (3 * rot)) | (wa.pl_pack << (24 - 3 * rot))) & 0xFFFFFFu;
     const uint32_t e_rot = ((wa.e_iota >> rot) | (wa.e_iota << (8 - rot))) & 0xFFu;
     PlaneSteps ps;
+    ps.one = one;
 #pragma unroll
     for (uint32_t q = 0; q < 8; ++q) {
       ps.pb[q] = img0 + 4 * ((pl_rot >> (3 * q)) & 7u);
@@ -1142,6 +1156,10 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
 #endif
     }
     while (q_cur < n_q) {
+      // issued and read in the same iteration: the asm output is written when
+      // the LDS returns it, so the value must not be live across a loop phi
+      // (a register copy there reads it early; a claim carried from one
+      // iteration into the next gave wrong counts)
       const uint32_t c2 = claim();  // unit after next, read at the end of this one
       if (q_nxt < n_q && unit_of(q_nxt) != ~0u && is_l(unit_of(q_nxt))) {
         load_L(nxt, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_nxt)) + lane, i_big);
@@ -1160,7 +1178,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
             e[t] = j + 64 * t < end ? __builtin_nontemporal_load(wa.bk_entries + j + 64 * t) : 0u;
 #pragma unroll
           for (uint32_t t = 0; t < kBkBatchU; ++t)
-            if (j + 64 * t < end) mark_plane<false>(img0 + 4 * (e[t] >> kWheelLogKP), e[t] & (KP - 1));
+            if (j + 64 * t < end) mark_plane<false>(img0 + 4 * (e[t] >> kWheelLogKP), e[t] & (KP - 1), one);
         }
         cur = nxt;
 #if DSE_L_SETS == 2
@@ -1182,12 +1200,12 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
           const uint32_t p = pi & 0xFFFFu;
           const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mid_m[k] >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_mid_m[k]);
-          if ((phases & kPhaseMidA) && (uint64_t)p * p < Vend) unit_A(img, pi, m, Vs, wa.rho_pack, lane);
+          if ((phases & kPhaseMidA) && (uint64_t)p * p < Vend) unit_A(img, pi, m, Vs, wa.rho_pack, lane, one);
         } else {
           const uint32_t j0 = nA + (k - nA) * 8;
           const uint32_t pf = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
           if ((phases & kPhaseMidB) && (uint64_t)pf * pf < Vend)
-            unit_B(img, s_mid_p, s_mid_m, j0, min(8u, n_mid - j0), Vs, Vend, wa.rho_pack, lane);
+            unit_B(img, s_mid_p, s_mid_m, j0, min(8u, n_mid - j0), Vs, Vend, wa.rho_pack, lane, one);
         }
       } else {
         const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p);

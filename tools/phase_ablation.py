@@ -7,7 +7,8 @@ N = sys.argv[1] if len(sys.argv) > 1 else "1e11"
 # wheel kernel phases: 1 = A, 2 = B, 4 = L, 8 = patterns (init), 16 = store, 32 = expand, 64 = unit loop
 variants = {"all": 127, "no_store": 111, "only_A": 1 | 120, "only_B": 2 | 120, "only_L": 4 | 120,
             "init_units_expand_store": 120, "init_units_expand": 104, "init_units": 72, "init_expand": 40,
-            "init": 8, "nothing": 0}
+            "init": 8, "nothing": 0, "no_A": 126, "no_B": 125, "no_L": 123, "no_init": 119,
+            "no_expand_store": 79}
 for name, ph in variants.items():
     env = dict(os.environ, DSE_PHASES=str(ph),
                DSE_LIB=os.environ.get("DSE_LIB", os.path.join(ROOT, "variants", "libdse_knob.so")))

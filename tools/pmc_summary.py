@@ -50,7 +50,13 @@ def main():
                   "SQ_ACTIVE_INST_LDS", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_VMEM"):
             if k in v:
                 print(f"{k + ' / WAVE_CYCLES':28s} {v[k] / wc:.3f}")
-    for lvl, n in (("SQ_INST_LEVEL_LDS", "SQ_INSTS_LDS"), ("SQ_INST_LEVEL_VMEM", "SQ_INSTS_VMEM_RD")):
+    if "SQC_ICACHE_HITS" in v and "SQC_ICACHE_MISSES" in v:
+        h, m = v["SQC_ICACHE_HITS"], v["SQC_ICACHE_MISSES"]
+        print(f"{'icache miss rate':28s} {m / max(h + m, 1):.4f}")
+    if cyc and "SQC_ICACHE_BUSY_CYCLES" in v:
+        print(f"{'icache busy per SQC-cycle':28s} {v['SQC_ICACHE_BUSY_CYCLES'] / (NUM_CUS / 2) / cyc:.3f} (one SQC per 2 CUs)")
+    for lvl, n in (("SQ_INST_LEVEL_LDS", "SQ_INSTS_LDS"), ("SQ_INST_LEVEL_VMEM", "SQ_INSTS_VMEM_RD"),
+                   ("SQ_IFETCH_LEVEL", "SQ_IFETCH")):
         if lvl in v and n in v and v[n]:
             print(f"{lvl + ' / ' + n:28s} {v[lvl] / v[n]:.1f} (avg latency, level units)")
     if "FETCH_SIZE" in v and "WRITE_SIZE" in v:
