@@ -147,10 +147,37 @@ def pmc_summary(N: int, P: int, window: bool):
                     "valu_issue_per_cu_cycle": v["SQ_INSTS_VALU"] / work.NUM_CUS / cyc,
                     "valu_frac": v["SQ_INSTS_VALU"] / work.NUM_CUS / cyc / work.VALU_PEAK_PER_CU_CYCLE,
                     "lds_busy": v["SQ_LDS_IDX_ACTIVE"] / work.NUM_CUS / cyc,
-                    "lds_conflict_share": v["SQ_LDS_BANK_CONFLICT"] / v["SQ_LDS_IDX_ACTIVE"]}
+                    "lds_conflict_share": v["SQ_LDS_BANK_CONFLICT"] / v["SQ_LDS_IDX_ACTIVE"],
+                    "sq_insts_lds": v["SQ_INSTS_LDS"]}
         except (OSError, KeyError, ZeroDivisionError):
             continue
     return None
+
+
+def lds_instr_check(wm: int, cs: int, pmc):
+    """The analytic executed-mark count against the PMC's LDS wave-instructions
+    per launch: SQ_INSTS_LDS = the marks (wm / 64 full-wave ds_or_b32) + the
+    expansion and init instructions, which the kernel's structure fixes per
+    segment (expand: 2 ds_read_b128 + 32 LUT ds_read_b32 per lane-row, 4,096
+    lane-rows; init: 7 x 9 ds_read_b128 table reads + 32 ds_write_b32 per lane,
+    1,024 lanes; csrc/dse_wheel.hip expand_segment / init_segment) + a rest:
+    unit claims and the ds_or of predicated marks issued with part of the wave
+    (A-class and B tails, L planes with <= 2 hits), which the analytic count
+    of hits cannot see: ~2.3 K wave-instructions per segment at N=1e11
+    (DESIGN.md section 6), 11% of the total. A negative rest, or one far above
+    that, would mean the analytic count is off. (A half-geometry tail segment
+    has half the lane-rows and 51 instead of 95 init instructions per lane:
+    counted here as full segments, < 0.1% at N=1e11.)"""
+    if not pmc:
+        return None
+    nseg = -(-cs // work.WHEEL_OUT_BITS)
+    mark_i = wm / 64
+    expand_i = nseg * (4096 // 64) * 34
+    init_i = nseg * (1024 // 64) * (7 * 9 + 32)
+    rest = pmc["sq_insts_lds"] - mark_i - expand_i - init_i
+    return {"sq_insts_lds": pmc["sq_insts_lds"], "marks_analytic": mark_i, "expand": expand_i, "init": init_i,
+            "rest": rest, "rest_share": rest / pmc["sq_insts_lds"],
+            "unit": "LDS wave-instructions per launch"}
 
 
 def main():
@@ -326,6 +353,10 @@ def main():
                 "lds_busy": pmc["lds_busy"] if pmc else None,
                 "lds_conflict_share": pmc["lds_conflict_share"] if pmc else None,
                 "pmc_source": pmc["source"] if pmc else None,
+                "executed_marks_source": "analytic (mail_sieve_e/work.py wheel_marks_for_range: multiples p*m >= p^2 "
+                                         "with gcd(m, 30) = 1 of the primes 61 < p <= sqrt(N)), cross-checked "
+                                         "against SQ_INSTS_LDS in lds_instr_check",
+                "lds_instr_check": lds_instr_check(wm, cs, pmc),
             }
         if world == 1 and a.cpu_baseline == "on" and not a.window:
             out["cpu_baseline"] = cpu_baseline(int(a.cpu_max_n))

@@ -80,6 +80,9 @@ static_assert(NE >= 1 && NE <= NW && (DSE_PIPELINE ? NE < NW : NE == NW) && ROWS
 #ifndef DSE_L_SETS
 #define DSE_L_SETS 2  // sets of 64 primes per L unit (A/B)
 #endif
+#ifndef DSE_B_PRED_EXEC
+#define DSE_B_PRED_EXEC 1  // 0: predicated-off A-class and B-tail marks OR 0 inside the image (A/B)
+#endif
 #ifndef DSE_WHEEL_HALF_TU
 #define DSE_WHEEL_HALF_TU 0  // 1: compiled by dse_wheel_half.hip with 2^16 periods per segment
 #endif
@@ -231,7 +234,7 @@ struct WheelArgs {
   uint16_t v0g[kNG];   // V0 mod M_G (init tables)
   uint32_t nthr[4];    // odd primes <= 61, <= TA, <= TB, <= kWheelMaxPrime (table indices of the unit lists)
   const uint32_t* bk_entries;  // bucketed hits of the primes > kWheelMaxPrime (or null):
-  const uint32_t* bk_start;    // segment s owns entries [bk_start[s], bk_start[s+1]), k | plane << kWheelLogKP
+  const uint32_t* bk_start;    // segment s owns entries [bk_start[s], bk_start[s+1]) (bucket_entry)
 };
 
 __device__ __forceinline__ void lds_or(uint32_t* a, uint32_t v) {
@@ -309,9 +312,14 @@ __device__ __forceinline__ uint32_t mark_run(uint32_t cb, uint32_t off, uint32_t
   return off;
 }
 
-// Mark period `off` of the column at byte address cb if off < LS (else an OR
-// of 0 at a row inside the column); returns the offset of the next hit.
+// Mark period `off` of the column at byte address cb if off < LS; returns the
+// offset of the next hit. A lane without the hit leaves the ds_or (exec mask:
+// no bit select, and idle lanes take no part in bank conflicts).
 __device__ __forceinline__ uint32_t mark_col_pred(uint32_t cb, uint32_t off, uint32_t p, uint32_t one) {
+#if DSE_B_PRED_EXEC
+  if (off < LS) mark_col_step(cb, off, p, one);
+  return off;
+#endif
   const bool hit = off < LS;
   const uint32_t bit = hit ? shl1(off, one) : 0u;
   uint32_t a;
@@ -499,7 +507,11 @@ __device__ __forceinline__ void a_classes(uint32_t img0, uint32_t cb_col, uint32
       a += D;
     }
     const bool in = a < img0 + IMG_BYTES;
+#if DSE_B_PRED_EXEC
+    if (in) mark_at(a, bit);  // exec mask, as mark_col_pred
+#else
     mark_at((a & (IMG_BYTES - 1)) | img0, in ? bit : 0u);
+#endif
     off = opaque(off + p);
   }
 }
@@ -639,6 +651,21 @@ __device__ __forceinline__ void mark_plane(uint32_t pb4, uint32_t kk, uint32_t o
       : "memory");
 }
 
+// Mark a bucketed hit: entry = LDS word index << 5 | bit (bucket_entry), so
+// the address is img0 + (e >> 5) * 4 and the bit 1 << (e & 31) (the shift reads the
+// low 5 bits itself): 3 VALU, where a (k, plane) entry took 8.
+__device__ __forceinline__ void mark_entry(uint32_t img0, uint32_t e, uint32_t one) {
+  uint32_t a, b;
+  asm volatile(
+      "v_lshrrev_b32 %0, 3, %2\n\t"
+      "v_and_or_b32 %0, %0, -4, %4\n\t"
+      "v_lshlrev_b32 %1, %2, %3\n\t"
+      "ds_or_b32 %0, %1"
+      : "=&v"(a), "=&v"(b)
+      : "v"(e), "v"(one), "v"(img0)
+      : "memory");
+}
+
 // L: 64 large primes (p > TB), one per lane; at step q lane L handles the
 // absolute residue (q + L) & 7 (a half-wave spreads over all 8 planes). The
 // per-plane hit count is at most ceil(KP / pmin): units whose primes all
@@ -652,6 +679,26 @@ struct PlaneSteps {
   uint32_t one;  // 1 in a VGPR (shl1)
 };
 
+#ifndef DSE_L_ADD3
+#define DSE_L_ADD3 1  // 0: plane starts as the compiler's add/sub/add/min (4 VALU) (A/B)
+#endif
+// Plane start (a - Kb - e) mod p = min(t, t + p), t = a + (-Kb mod p) + (-e)
+// as one v_add3 (left to itself the compiler forms a - (kbm + e): 4 VALU).
+__device__ __forceinline__ uint32_t plane_start(uint32_t a, uint32_t nKbm, uint32_t ne, uint32_t p) {
+#if DSE_L_ADD3
+  uint32_t t, u;
+  asm("v_add3_u32 %0, %2, %3, %4\n\t"
+      "v_add_u32 %1, %0, %5\n\t"
+      "v_min_u32 %0, %0, %1"
+      : "=&v"(t), "=&v"(u)
+      : "v"(a), "v"(nKbm), "v"(ne), "v"(p));
+  return t;
+#else
+  const uint32_t t = a + nKbm + ne;
+  return min(t, t + p);
+#endif
+}
+
 // Branch-free body of an L unit whose 64 primes are all live and past p^2
 // (the common case): the mark count per plane is decided once per unit.
 // MODE 2: pmin > KP, one predicated mark per plane; MODE 1: pmin > KP/2, two;
@@ -662,8 +709,7 @@ __device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, co
   const uint32_t p = o.p;
 #pragma unroll
   for (uint32_t q = 0; q < 8; ++q) {
-    const uint32_t t = o.a[q] + nKbm + ps.ne[q];
-    uint32_t kk = min(t, t + p);  // plane start (a - Kb - e) mod p
+    uint32_t kk = plane_start(o.a[q], nKbm, ps.ne[q], p);
     const uint32_t pb4 = ps.pb[q];
     if (MODE == 2) {
       mark_plane<true>(pb4, kk, ps.one);
@@ -724,8 +770,7 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
   // an address inside the image (mark_plane<true>).
 #pragma unroll
   for (uint32_t q = 0; q < 8; ++q) {
-    const uint32_t t = o.a[q] + nKbm + ps.ne[q];
-    uint32_t kk = min(t, t + p);  // plane start (a - Kb - e) mod p
+    uint32_t kk = plane_start(o.a[q], nKbm, ps.ne[q], p);
     if (slow) {
       const uint32_t pl = (pl_rot >> (3 * q)) & 7u;
       const uint32_t rho = (uint32_t)(rho_pack >> (5 * pl)) & 31u;
@@ -762,11 +807,11 @@ __device__ __attribute__((noinline)) void mark_bucket_hits(const uint32_t* __res
 #pragma unroll
     for (uint32_t q = 0; q < kBkBatch; ++q) e[q] = __builtin_nontemporal_load(ent + j + q * T);
 #pragma unroll
-    for (uint32_t q = 0; q < kBkBatch; ++q) mark_plane<false>(img0 + 4 * (e[q] >> kWheelLogKP), e[q] & (KP - 1), one);
+    for (uint32_t q = 0; q < kBkBatch; ++q) mark_entry(img0, e[q], one);
   }
   for (; j < b1; j += T) {
     const uint32_t e = ent[j];
-    mark_plane<false>(img0 + 4 * (e >> kWheelLogKP), e & (KP - 1), one);
+    mark_entry(img0, e, one);
   }
 }
 
@@ -1178,7 +1223,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
             e[t] = j + 64 * t < end ? __builtin_nontemporal_load(wa.bk_entries + j + 64 * t) : 0u;
 #pragma unroll
           for (uint32_t t = 0; t < kBkBatchU; ++t)
-            if (j + 64 * t < end) mark_plane<false>(img0 + 4 * (e[t] >> kWheelLogKP), e[t] & (KP - 1), one);
+            if (j + 64 * t < end) mark_entry(img0, e[t], one);
         }
         cur = nxt;
 #if DSE_L_SETS == 2
@@ -1359,7 +1404,7 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
 // such a prime hits a 2 M-integer segment less than once, so instead of
 // visiting every (prime, segment) pair the kernels below walk each prime's
 // multiples p*m, gcd(m, 30) = 1, across the whole range once and file every
-// hit under its segment: k | plane << kWheelLogKP. Two identical walks: count (LDS
+// hit under its segment (bucket_entry). Two identical walks: count (LDS
 // per-segment counters -> per-workgroup column), then fill (LDS cursors
 // seeded from the scanned columns). The wheel kernel ORs its segment's list.
 // ---------------------------------------------------------------------------
@@ -1460,13 +1505,19 @@ __device__ __forceinline__ uint64_t bucket_first(uint32_t p, uint64_t m, const B
   return (uint64_t)p * (m0 + d) - ba.V0;
 }
 
-// The hit at offset o (< span): its segment and entry k | plane << kWheelLogKP.
+// The hit at offset o (< span): its segment s and entry = the LDS word index
+// of (period k, plane) in the wheel kernel's image << 5 | k & 31, i.e. the
+// address and bit the wheel kernel ORs, decoded here where the walk has VALU
+// to spare (the fill kernels are bound by their stores), not in the wheel
+// kernel (mark_entry). Word index = row * 64 + 8 * column + plane < 2^15, so
+// an entry is < 2^20.
 __device__ __forceinline__ uint32_t bucket_entry(uint64_t o, const BucketArgs& ba, uint32_t& s) {
   s = ((uint32_t)(o >> kWheelLogKP)) / 30u;  // o < 2^34
   const uint32_t u = (uint32_t)(o - (uint64_t)s * kWheelSpan);
   const uint32_t k = u / 30u, rho = u - 30u * k;
   const uint32_t pl = (uint32_t)(ba.plane_lut >> (3 * (rho >> 1))) & 7u;
-  return k | (pl << kWheelLogKP);
+  const uint32_t word = (((k >> 5) & (ROWS - 1)) << 6) | ((k >> LOG_LS) << 3) | pl;
+  return (word << 5) | (k & 31u);
 }
 
 #ifndef DSE_BK_SNAKE
@@ -1660,8 +1711,8 @@ __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const 
 constexpr uint32_t kSupLog = 7;
 constexpr uint32_t kSupSegs = 1u << kSupLog;       // segments per super-bucket
 constexpr uint32_t kStageCap = 64;                 // keys per (wave, super-bucket) stage: one 256 B run
-constexpr uint32_t kKeyShift = 20;                 // entry = k | plane << 17 < 2^20
-static_assert(kWheelLogKP + 3 <= (int)kKeyShift && kKeyShift + kSupLog <= 32, "bucket key layout");
+constexpr uint32_t kKeyShift = 20;                 // entry = LDS word index << 5 | bit < 2^20
+static_assert(IMG_WORDS * 32 <= (1u << kKeyShift) && kKeyShift + kSupLog <= 32, "bucket key layout");
 #ifndef DSE_BK_SORT_GROUP
 #define DSE_BK_SORT_GROUP 16
 #endif

@@ -61,6 +61,7 @@ def marks_for_range(g_start: int, nbits: int) -> int:
 
 
 R30 = (1, 7, 11, 13, 17, 19, 23, 29)
+WHEEL_OUT_BITS = 15 * 2**17  # odd candidates per wheel-kernel segment (csrc/dse_internal.h kWheelOutBits)
 WHEEL_PATTERN_MAX = 61  # the wheel kernel ORs register patterns for 7..61 (no LDS marks)
 
 

@@ -1,8 +1,5 @@
-"""Print a rocprofv3 kernel_stats.csv as short name / calls / average ms (profiling aid)."""
-import csv, sys
-for f in sys.argv[1:]:
-    print("==", f)
-    for r in csv.DictReader(open(f)):
-        n = r["Name"].replace("(anonymous namespace)", "")
-        short = n.split("(")[0].split("::")[-1] if "(" in n else n
-        print(f"  {short:32s} calls={r['Calls']:>4s} avg_ms={float(r['AverageNs'])/1e6:8.3f} total_ms={float(r['TotalDurationNs'])/1e6:8.3f}")
+"""Print a rocprofv3 kernel_stats.csv compactly: short kernel name, calls, average us, total share."""
+import csv, re, sys
+for row in list(csv.DictReader(open(sys.argv[1])))[: int(sys.argv[2]) if len(sys.argv) > 2 else 12]:
+    name = re.sub(r"\(.*", "", row["Name"].replace("dse::(anonymous namespace)::", ""))
+    print(f"{name:32s} calls={row['Calls']:>4s} avg_us={float(row['AverageNs'])/1e3:9.1f} pct={float(row['Percentage']):6.2f}")
