@@ -622,6 +622,11 @@ int32_t dse_debug_set_option(dse_ctx* ctx, const char* name, int64_t value) {
     ctx->opts.wheel_geometry = (uint32_t)value;
     return DSE_OK;
   }
+  if (n == "bucket_k0_divisor") {
+    if (value < 0 || value > 0xFFFFFFFFll) return fail(DSE_EINVAL, "bucket_k0_divisor out of range");
+    ctx->opts.bucket_k0_div = (uint32_t)value;
+    return DSE_OK;
+  }
   if (n == "bucket_cap_divisor") {
     if (value < 0 || value > 0xFFFFFFFFll) return fail(DSE_EINVAL, "bucket_cap_divisor out of range");
     ctx->opts.bucket_cap_div = (uint32_t)value;

@@ -74,7 +74,8 @@ hipError_t free_scratch(Scratch* s);
 struct SieveOpts {
   uint32_t bucket_pass_segs = 0;  // > 0: cap the segments per bucket pass (multi-pass coverage)
   uint32_t bucket_split_log2 = 0; // > 0: bucketed primes <= 2^k filled one level, above two levels (0: production)
-  uint32_t bucket_cap_div = 0;    // > 1: divide the (rigorous) bucket entry capacity, to test the overflow flag
+  uint32_t bucket_cap_div = 0;    // > 1: divide the (rigorous) bucket entry capacities, to test the overflow flag
+  uint32_t bucket_k0_div = 0;     // > 1: divide the band-0 region capacity, to test the spill list
   uint32_t wheel_geometry = 0;    // ranges without buckets: 0 auto (half-size tail), 1 full only, 2 half only
 };
 

@@ -143,8 +143,8 @@ constexpr uint32_t kQInv30[kNQ] = {inv30_const(7),  inv30_const(11), inv30_const
 #ifndef DSE_BK_NO_M
 #define DSE_BK_NO_M 1  // 0: bucket walks read m[] (Barrett factors of every table prime) (A/B)
 #endif
-#ifndef DSE_BK_UNITS
-#define DSE_BK_UNITS 1  // 0: bucketed hits marked by every wave before the units (A/B)
+#ifndef DSE_BK_GRID
+#define DSE_BK_GRID 1024  // band-0 fill workgroups (columns)
 #endif
 #ifndef DSE_BK_UNIT_BATCHES
 #define DSE_BK_UNIT_BATCHES 4
@@ -233,8 +233,16 @@ struct WheelArgs {
   uint8_t v0q[kNQ];    // V0 mod q
   uint16_t v0g[kNG];   // V0 mod M_G (init tables)
   uint32_t nthr[4];    // odd primes <= 61, <= TA, <= TB, <= kWheelMaxPrime (table indices of the unit lists)
-  const uint32_t* bk_entries;  // bucketed hits of the primes > kWheelMaxPrime (or null):
-  const uint32_t* bk_start;    // segment s owns entries [bk_start[s], bk_start[s+1]) (bucket_entry)
+  // Bucketed hits of the primes > kWheelMaxPrime (bk_start null: none), as
+  // entries (bucket_entry):
+  const uint32_t* bk_entries;  // band 1: segment s owns [bk_start[s], bk_start[s+1])
+  const uint32_t* bk_start;
+  const uint32_t* bk_reg0;     // band 0: segment s, column b: bk_n0[s * kBucketGrid + b] entries
+  const uint32_t* bk_n0;       //   from bk_reg0 + (s * kBucketGrid + b) * bk_k0
+  const unsigned long long* bk_spill;  // band-0 hits past their region: segment << 32 | entry,
+  const uint32_t* bk_nspill;           //   *bk_nspill of them (normally none)
+  uint64_t bk_spill_cap;               //   (at most this many stored)
+  uint32_t bk_k0;              // band-0 region capacity (0: no band 0 in the pass)
 };
 
 __device__ __forceinline__ void lds_or(uint32_t* a, uint32_t v) {
@@ -793,30 +801,11 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
   }
 }
 
-// Bucketed hits of segment s (entries [b0, b1), thread t of T takes every
-// T-th): kBkBatch loads in flight per thread before their marks (one at a
-// time, every entry paid a full global-load latency: the window's wheel
-// kernel spent most of its time here). Not inlined: its registers stay out
-// of the unit loop's allocation.
-__device__ __attribute__((noinline)) void mark_bucket_hits(const uint32_t* __restrict__ ent, uint32_t b0, uint32_t b1,
-                                                         uint32_t t, uint32_t T, uint32_t img0, uint32_t one) {
-  constexpr uint32_t kBkBatch = 16;
-  uint32_t j = b0 + t;
-  for (; j + (kBkBatch - 1) * T < b1; j += kBkBatch * T) {
-    uint32_t e[kBkBatch];
-#pragma unroll
-    for (uint32_t q = 0; q < kBkBatch; ++q) e[q] = __builtin_nontemporal_load(ent + j + q * T);
-#pragma unroll
-    for (uint32_t q = 0; q < kBkBatch; ++q) mark_entry(img0, e[q], one);
-  }
-  for (; j < b1; j += T) {
-    const uint32_t e = ent[j];
-    mark_entry(img0, e, one);
-  }
-}
-
 constexpr uint32_t kBkBatchU = 16;                                // loads in flight per lane (bucket unit)
-constexpr uint32_t kBkUnit = 64 * kBkBatchU * DSE_BK_UNIT_BATCHES;  // entries per bucket unit
+constexpr uint32_t kBkUnit = 64 * kBkBatchU * DSE_BK_UNIT_BATCHES;  // band-1 entries per bucket unit
+constexpr uint32_t kBkGrid0 = DSE_BK_GRID;                         // band-0 columns (fill workgroups)
+constexpr uint32_t kBk0Lists = 16;                                 // band-0 columns per bucket unit
+static_assert(kBkGrid0 % kBk0Lists == 0 && 64 % kBk0Lists == 0, "band-0 bucket units");
 
 struct WheelLds {
   uint32_t img[NIMG][IMG_WORDS];   // the segment image(s), at LDS address 0
@@ -1124,23 +1113,20 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     asm volatile("" : "+v"(lane));
     const uint32_t img0 = lds_addr(img);
     const uint32_t one = opaque(1u);
-    // bucketed hits of the primes > kWheelMaxPrime: one entry per marking
-    // thread (pipelined: the non-expander waves)
-#if DSE_BK_UNITS
-    // bucketed hits as units of the queue (kBkUnit entries each), interleaved
-    // with the marking units, so their global-load latency overlaps other
-    // waves' marking instead of stalling every wave at the segment start
-    uint32_t bk_b0 = 0, n3 = 0;
+    // Bucketed hits of the primes > kWheelMaxPrime as units of the queue,
+    // interleaved with the marking units, so their global-load latency
+    // overlaps other waves' marking instead of stalling every wave at the
+    // segment start: n0u band-0 units (kBk0Lists columns each), then band-1
+    // units of kBkUnit entries, then one unit over the spill list if it is
+    // not empty.
+    uint32_t bk_b0 = 0, bk_b1 = 0, n0u = 0, n1u = 0, n3 = 0;
     if (wa.bk_start && (phases & kPhaseLarge)) {
+      n0u = wa.bk_k0 ? kBkGrid0 / kBk0Lists : 0u;
       bk_b0 = wa.bk_start[s];
-      n3 = (wa.bk_start[s + 1] - bk_b0 + kBkUnit - 1) / kBkUnit;
+      bk_b1 = wa.bk_start[s + 1];
+      n1u = (bk_b1 - bk_b0 + kBkUnit - 1) / kBkUnit;
+      n3 = n0u + n1u + (wa.bk_k0 && *wa.bk_nspill ? 1u : 0u);
     }
-    const uint32_t bk_b1 = n3 ? wa.bk_start[s + 1] : 0u;
-#else
-    constexpr uint32_t kMarkT0 = DSE_PIPELINE ? NE * 64 : 0;
-    if (wa.bk_start && (phases & kPhaseLarge) && tid >= kMarkT0)
-      mark_bucket_hits(wa.bk_entries, wa.bk_start[s], wa.bk_start[s + 1], tid - kMarkT0, NT - kMarkT0, img0, one);
-#endif
     const uint32_t rot = (i_mid1 + lane) & 7;  // = table index & 7 of this lane's large primes
     // absolute residue (q + rot) & 7 at step q: its plane and e bit
     const uint32_t pl_rot = ((wa.pl_pack >> (3 * rot)) | (wa.pl_pack << (24 - 3 * rot))) & 0xFFFFFFu;
@@ -1175,7 +1161,6 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     };
     auto is_l = [&](uint32_t u) -> bool { return u < 2 * n_int ? (u & 1) != 0 : n2 > n1; };
     auto idx_of = [&](uint32_t u) -> uint32_t { return u < 2 * n_int ? u >> 1 : u - n_int; };
-#if DSE_BK_UNITS
     // queue position -> marking unit (or ~0u: bucket unit bk_of(q)); the n3
     // bucket units interleave 1:1 with the marking units from the start
     const uint32_t mb = min(n3, n_all), n_q = n_all + n3;
@@ -1184,10 +1169,6 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       return n3 > n_all ? ~0u : q - mb;
     };
     auto bk_of = [&](uint32_t q) -> uint32_t { return q < 2 * mb ? q >> 1 : q - mb; };
-#else
-    const uint32_t n_q = n_all;
-    auto unit_of = [&](uint32_t q) -> uint32_t { return q; };
-#endif
     LargeOps cur, nxt;
 #if DSE_L_SETS == 2
     LargeOps cur1, nxt1;  // the unit's second 64 primes
@@ -1213,17 +1194,52 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
 #endif
       }
       const uint32_t u_cur = unit_of(q_cur);
-#if DSE_BK_UNITS
-      if (u_cur == ~0u) {  // a bucket unit: kBkUnit entries, kBkBatch loads in flight per lane
-        const uint32_t beg = bk_b0 + bk_of(q_cur) * kBkUnit, end = min(bk_b1, beg + kBkUnit);
-        for (uint32_t j = beg + lane; j < end; j += 64 * kBkBatchU) {
-          uint32_t e[kBkBatchU];
+      if (u_cur == ~0u) {  // a bucket unit, kBkBatchU loads in flight per lane
+        const uint32_t bu = bk_of(q_cur);
+        if (bu < n0u) {  // band 0: columns kBk0Lists bu .. +kBk0Lists, 4 at a time, each read by the whole wave
+          const uint64_t li0 = s * (uint64_t)kBkGrid0 + bu * kBk0Lists;
+          const uint32_t nl = lane < kBk0Lists ? wa.bk_n0[li0 + lane] : 0u;
+#pragma unroll 1
+          for (uint32_t g = 0; g < kBk0Lists; g += 4) {
+            uint32_t n[4], nmax = 0;
+            const uint32_t* __restrict__ r[4];
 #pragma unroll
-          for (uint32_t t = 0; t < kBkBatchU; ++t)
-            e[t] = j + 64 * t < end ? __builtin_nontemporal_load(wa.bk_entries + j + 64 * t) : 0u;
+            for (uint32_t l = 0; l < 4; ++l) {
+              n[l] = (uint32_t)__builtin_amdgcn_readlane((int)nl, (int)(g + l));
+              r[l] = wa.bk_reg0 + (li0 + g + l) * wa.bk_k0;
+              nmax = max(nmax, n[l]);
+            }
+            for (uint32_t o = lane; o < nmax + lane; o += 256) {  // contiguous 256-entry pieces of 4 lists
+              uint32_t e[16];
 #pragma unroll
-          for (uint32_t t = 0; t < kBkBatchU; ++t)
-            if (j + 64 * t < end) mark_entry(img0, e[t], one);
+              for (uint32_t l = 0; l < 4; ++l)
+#pragma unroll
+                for (uint32_t t = 0; t < 4; ++t)
+                  e[4 * l + t] = o + 64 * t < n[l] ? __builtin_nontemporal_load(r[l] + o + 64 * t) : 0u;
+#pragma unroll
+              for (uint32_t l = 0; l < 4; ++l)
+#pragma unroll
+                for (uint32_t t = 0; t < 4; ++t)
+                  if (o + 64 * t < n[l]) mark_entry(img0, e[4 * l + t], one);
+            }
+          }
+        } else if (bu < n0u + n1u) {  // band 1: kBkUnit entries of the segment's list
+          const uint32_t beg = bk_b0 + (bu - n0u) * kBkUnit, end = min(bk_b1, beg + kBkUnit);
+          for (uint32_t j = beg + lane; j < end; j += 64 * kBkBatchU) {
+            uint32_t e[kBkBatchU];
+#pragma unroll
+            for (uint32_t t = 0; t < kBkBatchU; ++t)
+              e[t] = j + 64 * t < end ? __builtin_nontemporal_load(wa.bk_entries + j + 64 * t) : 0u;
+#pragma unroll
+            for (uint32_t t = 0; t < kBkBatchU; ++t)
+              if (j + 64 * t < end) mark_entry(img0, e[t], one);
+          }
+        } else {  // the spill list (band-0 regions that overflowed): this segment's hits
+          const uint32_t ns = (uint32_t)min((uint64_t)*wa.bk_nspill, wa.bk_spill_cap);
+          for (uint32_t j = lane; j < ns; j += 64) {
+            const unsigned long long v = wa.bk_spill[j];
+            if ((uint32_t)(v >> 32) == (uint32_t)s) mark_entry(img0, (uint32_t)v, one);
+          }
         }
         cur = nxt;
 #if DSE_L_SETS == 2
@@ -1233,7 +1249,6 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         q_nxt = claimed(c2);
         continue;
       }
-#endif
       const uint32_t k = idx_of(u_cur);
 #ifdef DSE_TIMING
       const uint64_t t_u0 = __builtin_amdgcn_s_memtime();
@@ -1404,14 +1419,14 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
 // such a prime hits a 2 M-integer segment less than once, so instead of
 // visiting every (prime, segment) pair the kernels below walk each prime's
 // multiples p*m, gcd(m, 30) = 1, across the whole range once and file every
-// hit under its segment (bucket_entry). Two identical walks: count (LDS
-// per-segment counters -> per-workgroup column), then fill (LDS cursors
-// seeded from the scanned columns). The wheel kernel ORs its segment's list.
+// hit under its segment (bucket_entry). Band 0 (one level): each fill
+// workgroup files its hits into per-(segment, workgroup) regions of a fixed
+// capacity, overflow into a spill list. Band 1 (two levels): two identical
+// walks, count (LDS per-segment counters -> per-workgroup column) and stage
+// (regions from the scanned columns), then a sort by segment. The wheel
+// kernel ORs its segment's band-0 regions, band-1 list and spilled hits.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kBucketThreads = 256;
-#ifndef DSE_BK_GRID
-#define DSE_BK_GRID 1024
-#endif
 #ifndef DSE_BK_SEGS
 #define DSE_BK_SEGS 8192
 #endif
@@ -1420,12 +1435,10 @@ constexpr uint32_t kBucketThreads = 256;
 #endif
 // Two bands of bucketed primes: band 0 (p <= split, kBucketGrid workgroups)
 // is filled one level, band 1 (p > split, kBucketGrid1 workgroups) staged in
-// two levels. The count kernel's columns are the kBucketGrid + kBucketGrid1
-// "virtual workgroups", band 0 first, so within a segment band 0's entries
-// precede band 1's.
+// two levels; the count kernel's columns are band 1's workgroups.
 constexpr uint32_t kBucketGrid = DSE_BK_GRID;
 constexpr uint32_t kBucketGrid1 = DSE_BK_GRID1;
-constexpr uint32_t kBucketCols = kBucketGrid + kBucketGrid1;
+constexpr uint32_t kBucketCols = kBucketGrid1;
 static_assert(kBucketCols % 64 == 0, "column scan: whole lanes");
 constexpr uint32_t kBucketSplitLog = 25;           // production split: primes <= 2^25 one-level
 constexpr uint32_t kBucketMaxSegs = DSE_BK_SEGS; // segments per pass (LDS counters)
@@ -1441,6 +1454,18 @@ struct BucketArgs {
   uint32_t nseg;       // segments in the pass (<= kBucketMaxSegs)
   uint64_t vmax;       // largest value of the pass (primes with p^2 > vmax have no hits)
   uint64_t split;      // band 0: kWheelMaxPrime < p <= split, band 1: p > split
+};
+
+// Band-0 output of a pass (bucket_fill_wg).
+struct BandZero {
+  uint32_t* reg0;                  // [nseg][kBucketGrid][k0] regions
+  uint32_t* n0;                    // [nseg][kBucketGrid] region fills
+  unsigned long long* spill;       // segment << 32 | entry
+  uint32_t* nspill;                // spill list length
+  uint32_t k0;                     // region capacity
+  uint64_t spill_cap;              // spill list capacity (rigorous)
+  uint32_t* flag;                  // scratch flag[0] (sticky overflow) ...
+  unsigned long long* count;       // ... and bit 63 of the count, if the spill list overflows
 };
 
 // First index in [lo, hi) where the ascending table P has P[i] > bound (hi
@@ -1465,7 +1490,8 @@ __device__ uint32_t wave_upper_bound(const uint32_t* __restrict__ P, uint32_t lo
 // p^2 > vmax, range[2] = first with p > split (clamped to [range[0], range[1]]).
 // One wave.
 __global__ __launch_bounds__(64) void bucket_range_kernel(const void* __restrict__ table, uint64_t vmax,
-                                                          uint64_t split, uint32_t* __restrict__ range) {
+                                                          uint64_t split, uint32_t* __restrict__ range,
+                                                          uint32_t* __restrict__ nspill) {
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
   const uint32_t np = th->count == 0xFFFFFFFFu ? 0u : th->count;
   const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
@@ -1476,6 +1502,7 @@ __global__ __launch_bounds__(64) void bucket_range_kernel(const void* __restrict
     range[0] = i_lo;
     range[1] = i_hi;
     range[2] = i_sp;
+    *nspill = 0;  // the band-0 spill list of this pass
   }
 }
 
@@ -1580,11 +1607,9 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(const void
   const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
   for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) cnt[j] = 0;
   __syncthreads();
-  // workgroup x: column x, band 0 below kBucketGrid
-  const uint32_t band = blockIdx.x >= kBucketGrid;
-  const uint32_t i_lo = band ? range[2] : range[0], i_hi = band ? range[1] : range[2];
-  for_bucket_primes(P, M, i_lo, i_hi, blockIdx.x - band * kBucketGrid,
-                    (band ? kBucketGrid1 : kBucketGrid) * kBucketThreads, band == 0, [&](uint32_t p, uint64_t m) {
+  // band-1 workgroup x: column x
+  for_bucket_primes(P, M, range[2], range[1], blockIdx.x, kBucketGrid1 * kBucketThreads, false,
+                    [&](uint32_t p, uint64_t m) {
     bucket_walk(p, m, ba, [&](uint32_t sg, uint32_t) { atomicAdd(&cnt[sg], 1u); });
   });
   __syncthreads();
@@ -1660,30 +1685,47 @@ __global__ __launch_bounds__(1024) void bucket_startscan_kernel(const uint32_t* 
   }
 }
 
-// Band 0, one-level fill: every hit is one dword store at its slot (an LDS
-// cursor per segment). The lanes of a wave walk consecutive primes, so for
-// small p a step's hits share a segment and take consecutive slots (one
-// coalesced store); the larger the primes, the more a step's stores scatter
-// (2.7 ps per hit below 2^24, 12 ps above 2^28 at the 1e18 window), hence band 1.
+// Band 0, one-level fill: every hit is one dword store at its slot. Workgroup
+// b owns region (s, b) of every segment s: k0 slots at reg0 + (s kBucketGrid +
+// b) k0, slot = an LDS cursor per segment. No count pass: k0 bounds the
+// region's expected fill by many standard deviations (bucket_k0), and a hit
+// past it goes to the spill list (a global atomic; the list's capacity is a
+// rigorous bound on the band's hits), so nothing is dropped whatever k0 is.
+// The lanes of a wave walk consecutive primes, so for small p a step's hits
+// share a segment and take consecutive slots (one coalesced store); the
+// larger the primes, the more a step's stores scatter (2.7 ps per hit below
+// 2^24, 12 ps above 2^28 at the 1e18 window), hence band 1. At the end the
+// region fills go to n0[s kBucketGrid + b] (capped at k0).
 // (band-0 workgroup b; cur: nseg words of LDS)
 __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const void* __restrict__ table,
                                                const BucketArgs& ba, const uint32_t* __restrict__ range,
-                                               const uint32_t* __restrict__ cols, const uint32_t* __restrict__ start,
-                                               uint32_t* __restrict__ entries, uint64_t cap) {
+                                               const BandZero& bz) {
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
   const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
   const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
   const uint32_t i_lo = range[0], i_hi = range[2];
-  if (i_lo >= i_hi) return;
-  for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads)
-    cur[j] = start[j] + cols[(uint64_t)j * kBucketCols + b];
+  for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) cur[j] = 0;
   __syncthreads();
-  for_bucket_primes(P, M, i_lo, i_hi, b, kBucketGrid * kBucketThreads, true, [&](uint32_t p, uint64_t m) {
-    bucket_walk(p, m, ba, [&](uint32_t sg, uint32_t e) {
-      const uint32_t pos = atomicAdd(&cur[sg], 1u);
-      if (pos < cap) entries[pos] = e;
+  if (i_lo < i_hi) {
+    for_bucket_primes(P, M, i_lo, i_hi, b, kBucketGrid * kBucketThreads, true, [&](uint32_t p, uint64_t m) {
+      bucket_walk(p, m, ba, [&](uint32_t sg, uint32_t e) {
+        const uint32_t pos = atomicAdd(&cur[sg], 1u);
+        if (pos < bz.k0) {
+          bz.reg0[((uint64_t)sg * kBucketGrid + b) * bz.k0 + pos] = e;
+        } else {
+          const uint32_t j = atomicAdd(bz.nspill, 1u);
+          if (j < bz.spill_cap) {
+            bz.spill[j] = (unsigned long long)sg << 32 | e;
+          } else {  // only with a test-shrunk capacity (bucket_cap_divisor): fail loudly
+            bz.flag[0] = 1u;
+            atomicOr(bz.count, 1ull << 63);
+          }
+        }
+      });
     });
-  });
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) bz.n0[(uint64_t)j * kBucketGrid + b] = min(cur[j], bz.k0);
 }
 
 // Band 1, two-level fill: every global store is a run of consecutive dwords.
@@ -1694,7 +1736,7 @@ __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const 
 // from an LDS atomic) and writes a full stage as one 256 B run into its
 // workgroup's region of that super-bucket; the region of (band-1 workgroup g,
 // super-bucket S) starts at
-//   start[S kSupSegs] + sum over S's segments s of cols[s][kBucketGrid + g]
+//   start[S kSupSegs] + sum over S's segments s of cols[s][g]
 // (cols = per-segment exclusive scans over the virtual workgroups), so the
 // temporary array holds each super-bucket where its band-1 entries will end
 // up. A lane whose stage is full keeps its hit and retries after the flush.
@@ -1749,7 +1791,7 @@ __device__ __forceinline__ void bucket_stage_wg(uint32_t* sm, uint32_t b, const 
   for (uint32_t S = lane; S < nsup; S += 64) scnt[S] = 0;
   __syncthreads();
   for (uint32_t s = tid; s < ba.nseg; s += kBucketThreads)
-    atomicAdd(&cur[s >> kSupLog], cols[(uint64_t)s * kBucketCols + kBucketGrid + b]);
+    atomicAdd(&cur[s >> kSupLog], cols[(uint64_t)s * kBucketCols + b]);
   __syncthreads();
 
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
@@ -1826,13 +1868,13 @@ __device__ __forceinline__ void bucket_stage_wg(uint32_t* sm, uint32_t b, const 
 // latency-bound staging of the other share the CUs (and neither pays a tail).
 __global__ __launch_bounds__(kBucketThreads) void bucket_fill_stage_kernel(
     const void* __restrict__ table, BucketArgs ba, const uint32_t* __restrict__ range,
-    const uint32_t* __restrict__ cols, const uint32_t* __restrict__ start, uint32_t* __restrict__ entries,
-    uint64_t cap, uint32_t* __restrict__ tmp, uint32_t nsup, uint32_t nfill, const uint32_t* __restrict__ flag) {
+    const uint32_t* __restrict__ cols, const uint32_t* __restrict__ start, BandZero bz,
+    uint32_t* __restrict__ tmp, uint32_t nsup, uint32_t nfill, const uint32_t* __restrict__ flag) {
   extern __shared__ uint32_t sm[];
   if (flag[1]) return;  // capacity overflow (bucket_startscan_kernel)
   const uint32_t x = blockIdx.x;
   if (x < nfill)
-    bucket_fill_wg(sm, x, table, ba, range, cols, start, entries, cap);
+    bucket_fill_wg(sm, x, table, ba, range, bz);
   else
     bucket_stage_wg(sm, x - nfill, table, ba, range, cols, start, tmp, nsup);
 }
@@ -1850,7 +1892,7 @@ __global__ __launch_bounds__(kSortThreads) void bucket_sort_kernel(BucketArgs ba
   __shared__ uint32_t rb[2];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   constexpr uint32_t ngroups = kBucketGrid1 / kSortGroup;
-  const uint32_t S = blockIdx.x / ngroups, g0 = kBucketGrid + (blockIdx.x % ngroups) * kSortGroup,
+  const uint32_t S = blockIdx.x / ngroups, g0 = (blockIdx.x % ngroups) * kSortGroup,
                  g1 = g0 + kSortGroup;
   const uint32_t s0 = S << kSupLog;
   if (tid < 2) rb[tid] = 0;
@@ -2044,7 +2086,32 @@ uint64_t bucket_cap(uint64_t span, double a, double b) {
   return (uint64_t)(8.0 * (double)span / 30.0 * s + 8.0 * 1.25506 * b / lb) + 1024;
 }
 
-constexpr uint64_t kBucketMaxEntries = 1ull << 31;  // 8 GB of entries per pass
+// Band-0 region capacity k0 (bucket_fill_wg). A region collects the hits in one
+// segment of one fill workgroup's primes: 256 per stride round r, all >= the
+// round's first prime p(r), so its mean is at most lambda = (8 W / 30) sum_r
+// 256 / p(r) (p(r) from the table index i_lo + r S: p_n >= n (ln n + ln ln n
+// - 1), Dusart), and its variance at most lambda plus ~4 per prime below the
+// segment span W (~1 hit per prime there, +-2). k0 = lambda + 10 sigma + 64:
+// a region past it is a >10-sigma event, and even then its hits are spilled,
+// not lost.
+uint32_t bucket_k0(uint32_t i_lo, double a, double b) {
+  if (b <= a) return 0;
+  const double S = (double)kBucketGrid * kBucketThreads;
+  const double n_band = 1.25506 * b / __builtin_log(b) - (double)i_lo;  // >= the band's primes
+  const double mu = 8.0 * (double)kWheelSpan / 30.0;
+  double lam = 0;
+  for (double r = 0; r * S < n_band; r += 1) {
+    const double n = (double)i_lo + r * S + 2;  // 1-based index of the round's first prime (2 is p_1)
+    const double pl = std::max(a, n * (__builtin_log(n) + __builtin_log(__builtin_log(n)) - 1.0));
+    lam += mu * kBucketThreads / pl;
+  }
+  const double var = lam + 4.0 * kBucketThreads;
+  const uint64_t k0 = (uint64_t)(lam + 10.0 * __builtin_sqrt(var) + 64.0);
+  return (uint32_t)((k0 + 15) & ~15ull);
+}
+
+constexpr uint64_t kBucketMaxEntries = 1ull << 31;  // 8 GB of band-1 entries per pass
+constexpr uint64_t kBucketMaxRegionBytes = 24ull << 30;  // band-0 regions per pass
 
 // Grow the context's scratch to `bytes` for a pass on `stream`, ordered after
 // the previous pass whatever stream that ran on: a grow waits for it on the
@@ -2140,28 +2207,43 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
   const uint64_t total_seg = (nbits + kWheelOutBits - 1) / kWheelOutBits;
   uint64_t max_segs = kBucketMaxSegs;
   if (opts && opts->bucket_pass_segs >= 1 && opts->bucket_pass_segs < max_segs) max_segs = opts->bucket_pass_segs;
+  const uint64_t split = 1ull << (opts && opts->bucket_split_log2 ? opts->bucket_split_log2 : kBucketSplitLog);
+  const uint32_t cap_div = opts && opts->bucket_cap_div > 1 ? opts->bucket_cap_div : 1;  // test-only: overflow
+  const uint32_t k0_div = opts && opts->bucket_k0_div > 1 ? opts->bucket_k0_div : 1;     // test-only: spills
+  const double a0 = (double)kWheelMaxPrime, b0 = std::min((double)split, (double)root);  // band 0: (a0, b0]
   for (uint64_t s0 = 0; s0 < total_seg;) {
     uint64_t ns = std::min<uint64_t>(max_segs, total_seg - s0);
-    while (ns > 1 && bucket_cap(ns * kWheelSpan, (double)kWheelMaxPrime, (double)root) > kBucketMaxEntries) ns /= 2;
+    WheelArgs wa = make_wheel_args(g_start + s0 * kWheelOutBits, kWheelOutBits, &plane_lut);  // (wa.nthr)
+    const uint32_t k0_full = bucket_k0(wa.nthr[3], a0, b0);
+    while (ns > 1 && (bucket_cap(ns * kWheelSpan, (double)split, (double)root) > kBucketMaxEntries ||
+                      4ull * ns * kBucketGrid * k0_full > kBucketMaxRegionBytes))
+      ns /= 2;
     const uint64_t g0 = g_start + s0 * kWheelOutBits;
     const uint64_t nb = std::min<uint64_t>(nbits - s0 * kWheelOutBits, ns * kWheelOutBits);
     const uint64_t vmax_p = 3 + 2 * (g0 + nb - 1);
-    WheelArgs wa = make_wheel_args(g0, nb, &plane_lut);
+    wa = make_wheel_args(g0, nb, &plane_lut);
     BucketArgs ba{};
     ba.V0 = wa.V0;
     ba.span = ns * kWheelSpan;
     ba.plane_lut = plane_lut;
     ba.nseg = (uint32_t)ns;
     ba.vmax = vmax_p;
+    ba.split = split;
     const uint64_t root_p = isqrt64(vmax_p);
-    uint64_t cap = bucket_cap(ba.span, (double)kWheelMaxPrime, (double)root_p);
-    if (opts && opts->bucket_cap_div > 1) cap /= opts->bucket_cap_div;  // test-only: force the overflow path
-    ba.split = 1ull << (opts && opts->bucket_split_log2 ? opts->bucket_split_log2 : kBucketSplitLog);
-    const bool band0 = ba.split > kWheelMaxPrime, band1 = ba.split < root_p;
-    // scratch: [range 3][cols 2*grid*ns][tot ns][start ns+1][entries cap][band-1 level-1 keys cap]
+    const bool band0 = split > kWheelMaxPrime, band1 = split < root_p;
+    // band 1: rigorous entry capacity (its keys, then its sorted entries);
+    // band 0: regions of k0 slots per (segment, fill workgroup), the spill
+    // list's capacity a rigorous bound on the band's hits
+    const uint64_t cap = (band1 ? bucket_cap(ba.span, (double)split, (double)root_p) : 64) / cap_div;
+    const uint32_t k0 = band0 ? std::max<uint32_t>(1, k0_full / k0_div / cap_div) : 0;
+    const uint64_t spill_cap = band0 ? bucket_cap(ba.span, a0, std::min((double)split, (double)root_p)) / cap_div : 0;
+    // scratch: [range 3, nspill][cols grid1*ns][tot ns][start ns+1][entries cap][band-1 keys cap]
+    //          [band-0 regions ns*grid*k0][band-0 fills ns*grid][spill list (8 B) spill_cap]
+    auto al = [](uint64_t x) { return (x + 255) & ~255ull; };
     const uint64_t o_cols = 256, o_tot = o_cols + 4ull * kBucketCols * ns, o_start = o_tot + 4 * ns + 256,
-                   o_ent = (o_start + 4 * (ns + 1) + 255) & ~255ull, o_tmp = (o_ent + 4 * cap + 255) & ~255ull,
-                   bytes = band1 ? o_tmp + 4 * cap : o_ent + 4 * cap;
+                   o_ent = al(o_start + 4 * (ns + 1)), o_tmp = al(o_ent + 4 * cap),
+                   o_reg = al(band1 ? o_tmp + 4 * cap : o_tmp), o_n0 = al(o_reg + 4ull * ns * kBucketGrid * k0),
+                   o_spill = al(o_n0 + (band0 ? 4ull * ns * kBucketGrid : 0)), bytes = o_spill + 8 * spill_cap;
     char* sc = nullptr;
     hipError_t e = ensure_scratch(scratch, bytes, stream, &sc);
     if (e != hipSuccess) return e;
@@ -2171,8 +2253,17 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     uint32_t* start = reinterpret_cast<uint32_t*>(sc + o_start);
     uint32_t* ent = reinterpret_cast<uint32_t*>(sc + o_ent);
     uint32_t* tmp = reinterpret_cast<uint32_t*>(sc + o_tmp);
-    hipLaunchKernelGGL(bucket_range_kernel, dim3(1), dim3(64), 0, stream, table, vmax_p, ba.split, range);
-    hipLaunchKernelGGL(bucket_count_kernel, dim3(kBucketCols), dim3(kBucketThreads), 4 * (uint32_t)ns, stream, table,
+    BandZero bz{};
+    bz.reg0 = reinterpret_cast<uint32_t*>(sc + o_reg);
+    bz.n0 = reinterpret_cast<uint32_t*>(sc + o_n0);
+    bz.spill = reinterpret_cast<unsigned long long*>(sc + o_spill);
+    bz.nspill = range + 3;
+    bz.k0 = k0;
+    bz.spill_cap = spill_cap;
+    bz.flag = scratch->flag;
+    bz.count = count;
+    hipLaunchKernelGGL(bucket_range_kernel, dim3(1), dim3(64), 0, stream, table, vmax_p, ba.split, range, bz.nspill);
+    hipLaunchKernelGGL(bucket_count_kernel, dim3(kBucketGrid1), dim3(kBucketThreads), 4 * (uint32_t)ns, stream, table,
                        ba, range, cols);
     hipLaunchKernelGGL(bucket_colscan_kernel, dim3((uint32_t)((ns + 3) / 4)), dim3(256), 0, stream, cols,
                        (uint32_t)ns, tot);
@@ -2186,7 +2277,7 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes)) != hipSuccess)
       return e;
     hipLaunchKernelGGL(bucket_fill_stage_kernel, dim3(nfill + (band1 ? kBucketGrid1 : 0)), dim3(kBucketThreads),
-                       lds_bytes, stream, table, ba, range, cols, start, ent, cap, tmp, nsup, nfill, scratch->flag);
+                       lds_bytes, stream, table, ba, range, cols, start, bz, tmp, nsup, nfill, scratch->flag);
     if (band1) {
       hipLaunchKernelGGL(bucket_sort_kernel, dim3(nsup * (kBucketGrid1 / kSortGroup)), dim3(kSortThreads), 0,
                          stream, ba, cols, start, tmp, ent, scratch->flag);
@@ -2194,6 +2285,12 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     if ((e = hipGetLastError()) != hipSuccess) return e;
     wa.bk_entries = ent;
     wa.bk_start = start;
+    wa.bk_reg0 = bz.reg0;
+    wa.bk_n0 = bz.n0;
+    wa.bk_spill = bz.spill;
+    wa.bk_nspill = bz.nspill;
+    wa.bk_spill_cap = spill_cap;
+    wa.bk_k0 = k0;
     if ((e = launch_wheel(table, wa, out ? out + s0 * (kWheelOutBits / 32) : nullptr, count, num_cus, stream)) !=
         hipSuccess)
       return e;

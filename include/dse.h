@@ -188,8 +188,11 @@ int32_t dse_device_status(dse_ctx *ctx);
  *   "wheel_geometry" = 0 (default): a range's last partial round of full
  *   segments is sieved as half-size segments when that is faster; 1: full
  *   segments only; 2: half-size segments only (covers that kernel in tests).
- *   "bucket_cap_divisor" = d >= 0: divide each pass's bucket entry capacity
+ *   "bucket_cap_divisor" = d >= 0: divide each pass's bucket entry capacities
  *   by d (> 1), forcing the overflow path (DSE_EINTERNAL); 0 or 1 = default.
+ *   "bucket_k0_divisor" = d >= 0: divide the band-0 region capacity by d
+ *   (> 1), so hits go through the spill list (results unchanged); 0 or 1 =
+ *   default.
  * DSE_EINVAL for an unknown name or a value out of range. */
 int32_t dse_debug_set_option(dse_ctx *ctx, const char *name, int64_t value);
 

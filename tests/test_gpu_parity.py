@@ -426,7 +426,8 @@ def test_debug_option_rejects_unknown(ctx):
     with pytest.raises(_dse.DseError):
         ctx.debug_set_option("no_such_option", 1)
     for name, bad in (("bucket_split_log2", 64), ("bucket_split_log2", -1), ("bucket_pass_segments", -1),
-                      ("bucket_cap_divisor", -1), ("wheel_geometry", 3), ("wheel_geometry", -1)):
+                      ("bucket_cap_divisor", -1), ("bucket_k0_divisor", -1), ("wheel_geometry", 3),
+                      ("wheel_geometry", -1)):
         with pytest.raises(_dse.DseError):
             ctx.debug_set_option(name, bad)
 
@@ -465,6 +466,27 @@ def test_bucket_overflow_flag(oracle):
         c.debug_set_option("bucket_cap_divisor", 0)
         m, cnt2 = c.sieve_odd_range(g0, nb)
         assert cnt2 == c_ref and np.array_equal(m, m_ref)
+
+
+@pytest.mark.parametrize("div", [8, 100000])
+def test_bucket_spill_list(oracle, div):
+    """Band-0 regions shrunk (test-only option bucket_k0_divisor): hits past a
+    region's capacity go through the spill list, and masks and counts stay
+    exact. div=8 spills a region's tail, 100000 leaves one slot per region (every
+    other hit spilled); multi-pass (3-segment passes) with both bands."""
+    from mail_sieve_e import sieve as S
+    g0, nb = (10**15 + 1 - 3) // 2, 3 * 10**6
+    m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
+    with S.Context(num_gpus=1) as c:
+        c.debug_set_option("bucket_k0_divisor", div)
+        m, cnt = c.sieve_odd_range(g0, nb)
+        assert cnt == c_ref and np.array_equal(m, m_ref)
+        c.debug_set_option("bucket_split_log2", 22)
+        c.debug_set_option("bucket_pass_segments", 3)
+        g1, nb1 = (10**18 + 1 - 3) // 2, 10**7
+        m, cnt = c.sieve_odd_range(g1, nb1)
+        m_ref, c_ref = oracle.fast_sieve_range(g1, nb1)
+        assert cnt == c_ref and np.array_equal(m, m_ref)
 
 
 def test_scratch_null_stream_then_host_call(oracle):
