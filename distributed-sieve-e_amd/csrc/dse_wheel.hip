@@ -1440,7 +1440,10 @@ constexpr uint32_t kBucketGrid = DSE_BK_GRID;
 constexpr uint32_t kBucketGrid1 = DSE_BK_GRID1;
 constexpr uint32_t kBucketCols = kBucketGrid1;
 static_assert(kBucketCols % 64 == 0, "column scan: whole lanes");
-constexpr uint32_t kBucketSplitLog = 25;           // production split: primes <= 2^25 one-level
+#ifndef DSE_BK_SPLIT_LOG
+#define DSE_BK_SPLIT_LOG 26
+#endif
+constexpr uint32_t kBucketSplitLog = DSE_BK_SPLIT_LOG;  // production split: primes <= 2^26 one-level
 constexpr uint32_t kBucketMaxSegs = DSE_BK_SEGS; // segments per pass (LDS counters)
 constexpr uint32_t kCoprime30 = (1u << 1) | (1u << 7) | (1u << 11) | (1u << 13) | (1u << 17) | (1u << 19) |
                                 (1u << 23) | (1u << 29);
@@ -1685,6 +1688,14 @@ __global__ __launch_bounds__(1024) void bucket_startscan_kernel(const uint32_t* 
   }
 }
 
+#ifndef DSE_BK_CHUNK
+#define DSE_BK_CHUNK 32  // band-0 fill walks chunks of this many segments (0: prime by prime, A/B)
+#endif
+#ifndef DSE_BK_FILL_RG
+#define DSE_BK_FILL_RG 8
+#endif
+constexpr uint32_t kFillRG = DSE_BK_FILL_RG;  // stride rounds of primes walked together (DSE_BK_CHUNK)
+
 // Band 0, one-level fill: every hit is one dword store at its slot. Workgroup
 // b owns region (s, b) of every segment s: k0 slots at reg0 + (s kBucketGrid +
 // b) k0, slot = an LDS cursor per segment. No count pass: k0 bounds the
@@ -1706,24 +1717,65 @@ __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const 
   const uint32_t i_lo = range[0], i_hi = range[2];
   for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) cur[j] = 0;
   __syncthreads();
-  if (i_lo < i_hi) {
-    for_bucket_primes(P, M, i_lo, i_hi, b, kBucketGrid * kBucketThreads, true, [&](uint32_t p, uint64_t m) {
-      bucket_walk(p, m, ba, [&](uint32_t sg, uint32_t e) {
-        const uint32_t pos = atomicAdd(&cur[sg], 1u);
-        if (pos < bz.k0) {
-          bz.reg0[((uint64_t)sg * kBucketGrid + b) * bz.k0 + pos] = e;
-        } else {
-          const uint32_t j = atomicAdd(bz.nspill, 1u);
-          if (j < bz.spill_cap) {
-            bz.spill[j] = (unsigned long long)sg << 32 | e;
-          } else {  // only with a test-shrunk capacity (bucket_cap_divisor): fail loudly
-            bz.flag[0] = 1u;
-            atomicOr(bz.count, 1ull << 63);
-          }
+  auto emit = [&](uint32_t sg, uint32_t e) {
+    const uint32_t pos = atomicAdd(&cur[sg], 1u);
+    if (pos < bz.k0) {
+      bz.reg0[((uint64_t)sg * kBucketGrid + b) * bz.k0 + pos] = e;
+    } else {
+      const uint32_t j = atomicAdd(bz.nspill, 1u);
+      if (j < bz.spill_cap) {
+        bz.spill[j] = (unsigned long long)sg << 32 | e;
+      } else {  // only with a test-shrunk capacity (bucket_cap_divisor): fail loudly
+        bz.flag[0] = 1u;
+        atomicOr(bz.count, 1ull << 63);
+      }
+    }
+  };
+#if DSE_BK_CHUNK
+  // Segment-ordered walk: a thread walks its primes of kFillRG stride rounds
+  // together, chunk by chunk of DSE_BK_CHUNK segments, so region (s, b) gets
+  // its hits within one chunk's time (while its lines are still in the L2)
+  // instead of over the whole walk.
+  constexpr uint32_t stride = kBucketGrid * kBucketThreads;
+  const uint32_t j = b * kBucketThreads + threadIdx.x;
+  const uint32_t jr = DSE_BK_SNAKE ? stride - 1 - j : j;
+  const uint64_t chunk = (uint64_t)DSE_BK_CHUNK * kWheelSpan;
+  for (uint64_t r0 = 0; i_lo + r0 * stride < i_hi; r0 += kFillRG) {
+    uint64_t o[kFillRG];
+    uint32_t pr[kFillRG], w3[kFillRG];
+#pragma unroll
+    for (uint32_t r = 0; r < kFillRG; ++r) {
+      const uint64_t i = i_lo + (r0 + r) * stride + (((r0 + r) & 1) ? jr : j);
+      o[r] = ba.span;
+      pr[r] = 0;
+      w3[r] = 0;
+      if (i < i_hi) {
+        pr[r] = P[i];
+        o[r] = bucket_first(pr[r], DSE_BK_NO_M ? 0 : M[i], ba, w3[r]);
+      }
+    }
+    for (uint64_t end = chunk;; end += chunk) {
+      const uint64_t lim = min(end, ba.span);
+      bool left = false;
+#pragma unroll
+      for (uint32_t r = 0; r < kFillRG; ++r) {
+        while (o[r] < lim) {
+          uint32_t sg;
+          const uint32_t e = bucket_entry(o[r], ba, sg);
+          emit(sg, e);
+          o[r] += (uint64_t)pr[r] * ((kGap30 >> w3[r]) & 7u);
+          w3[r] = w3[r] == 21 ? 0u : w3[r] + 3;
         }
-      });
-    });
+        left |= o[r] < ba.span;
+      }
+      if (!left) break;
+    }
   }
+#else
+  if (i_lo < i_hi)
+    for_bucket_primes(P, M, i_lo, i_hi, b, kBucketGrid * kBucketThreads, true,
+                      [&](uint32_t p, uint64_t m) { bucket_walk(p, m, ba, emit); });
+#endif
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) bz.n0[(uint64_t)j * kBucketGrid + b] = min(cur[j], bz.k0);
 }

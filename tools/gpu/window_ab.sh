@@ -1,12 +1,8 @@
-#!/bin/bash
-# Window [1e18, 1e18+1e10] timing (tools/window_bench.py) for library variants, interleaved:
-#   OUT=gpurun_out/<dir> ROUNDS=2 bash tools/gpu/window_ab.sh prod bu ...
+# interleaved window timing of prod and variants, x3 (window_bench checks the count)
 set -o pipefail
-OUT=${OUT:-gpurun_out/wab}; mkdir -p $OUT
-for r in $(seq 1 ${ROUNDS:-2}); do
-  for v in "$@"; do
-    L=$([ "$v" = prod ] && echo distributed-sieve-e_amd/mail_sieve_e/libdse.so || echo variants/libdse_$v.so)
-    echo -n "$r $v: " | tee -a $OUT/window_ab.txt
-    DSE_LIB=$L timeout -k 10 120 python tools/window_bench.py 2>&1 | tail -1 | tee -a $OUT/window_ab.txt || exit 1
+for r in 1 2 3; do
+  for v in prod "$@"; do
+    if [ "$v" = prod ]; then L=""; else L=variants/libdse_$v.so; fi
+    echo -n "$v: "; DSE_LIB=$L timeout -k 10 120 python tools/window_bench.py || exit 1
   done
 done
