@@ -97,6 +97,10 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
 // last round of full segments would leave most CUs idle. No bucketed primes.
 hipError_t launch_wheel_range_half(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
                                    unsigned long long* count, int num_cus, hipStream_t stream);
+// The full-geometry wheel kernel without bucketed primes (dse_wheel_plain.hip,
+// its own compile flags); wa points at the caller's WheelArgs (dse_wheel.hip).
+hipError_t launch_wheel_plain(const void* table, const void* wa, uint32_t* out, unsigned long long* count,
+                              int num_cus, hipStream_t stream);
 // Fill the Barrett factors m[] and wheel offsets a[] of a table whose p[] is final.
 // n_hint: table capacity when known (sizes the grid: about 4 primes per thread)
 hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream, uint64_t n_hint = 0);

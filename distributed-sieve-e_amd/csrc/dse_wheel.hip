@@ -86,6 +86,10 @@ static_assert(NE >= 1 && NE <= NW && (DSE_PIPELINE ? NE < NW : NE == NW) && ROWS
 #ifndef DSE_WHEEL_HALF_TU
 #define DSE_WHEEL_HALF_TU 0  // 1: compiled by dse_wheel_half.hip with 2^16 periods per segment
 #endif
+#ifndef DSE_WHEEL_PLAIN_TU
+#define DSE_WHEEL_PLAIN_TU 0  // 1: compiled by dse_wheel_plain.hip: the no-bucket kernel only
+#endif
+#define DSE_WHEEL_MAIN_TU (!DSE_WHEEL_HALF_TU && !DSE_WHEEL_PLAIN_TU)
 #ifndef DSE_HALF_SEG_COST
 #define DSE_HALF_SEG_COST 0.68
 #endif
@@ -1368,7 +1372,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   }
 }
 
-#if !DSE_WHEEL_HALF_TU
+#if DSE_WHEEL_MAIN_TU
 // floor((2^64-1)/p) for 2 <= p < 2^32 without a 64-bit division: a double
 // quotient (relative error 2^-52, so off by < 2^11) corrected by the exact
 // remainder, itself below 2^43 in magnitude and so exact in a double.
@@ -2026,10 +2030,10 @@ __global__ __launch_bounds__(kSortThreads) void bucket_sort_kernel(BucketArgs ba
   }
 }
 
-#endif  // !DSE_WHEEL_HALF_TU
+#endif  // DSE_WHEEL_MAIN_TU
 }  // namespace
 
-#if !DSE_WHEEL_HALF_TU
+#if DSE_WHEEL_MAIN_TU
 hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream, uint64_t n_hint) {
   const uint64_t grid = std::max<uint64_t>(4 * (uint64_t)num_cus, std::min<uint64_t>(n_hint / 1024 + 1, 1u << 16));
   hipLaunchKernelGGL(wheel_offsets_kernel, dim3((uint32_t)grid), dim3(256), 0, stream, table);
@@ -2058,7 +2062,7 @@ hipError_t free_scratch(Scratch* s) {
   s->used = false;
   return e != hipSuccess ? e : f != hipSuccess ? f : g;
 }
-#endif  // !DSE_WHEEL_HALF_TU
+#endif  // DSE_WHEEL_MAIN_TU
 
 namespace {
 
@@ -2131,7 +2135,7 @@ uint64_t isqrt64(uint64_t x) {
   return r;
 }
 
-#if !DSE_WHEEL_HALF_TU
+#if DSE_WHEEL_MAIN_TU
 // Rigorous bound on the bucket entries of a pass spanning `span` integers with
 // primes in (a, b]: each prime has <= 8 span / (30 p) + 8 coprime multiples;
 // sum 1/p <= ln(ln b / ln a) + 1/ln^2 a and pi(b) <= 1.25506 b / ln b.
@@ -2201,22 +2205,35 @@ hipError_t release_scratch(Scratch* sc, hipStream_t stream) {
   return e;
 }
 
-#endif  // !DSE_WHEEL_HALF_TU
+#endif  // DSE_WHEEL_MAIN_TU
 
 hipError_t launch_wheel(const void* table, const WheelArgs& wa, uint32_t* out, unsigned long long* count,
                         int num_cus, hipStream_t stream) {
   const uint64_t nseg = (wa.nbits + kWheelOutBits - 1) / kWheelOutBits;
   const uint64_t grid = nseg < (uint64_t)num_cus ? nseg : (uint64_t)num_cus;
-  if (wa.bk_start)
-    hipLaunchKernelGGL(wheel_segments_kernel<true>, dim3((uint32_t)grid), dim3(NT), 0, stream, table, wa, out, count);
-  else
-    hipLaunchKernelGGL(wheel_segments_kernel<false>, dim3((uint32_t)grid), dim3(NT), 0, stream, table, wa, out, count);
+#if DSE_WHEEL_MAIN_TU
+  // ranges without bucketed primes: the no-bucket instantiation, compiled in
+  // dse_wheel_plain.hip with the default machine scheduler (its loop spills
+  // fewer SGPRs there; the bucket instantiation is faster with iterative-ILP)
+  if (!wa.bk_start) return launch_wheel_plain(table, &wa, out, count, num_cus, stream);
+  hipLaunchKernelGGL(wheel_segments_kernel<true>, dim3((uint32_t)grid), dim3(NT), 0, stream, table, wa, out, count);
+#else
+  hipLaunchKernelGGL(wheel_segments_kernel<false>, dim3((uint32_t)grid), dim3(NT), 0, stream, table, wa, out, count);
+#endif
   return hipGetLastError();
 }
 
 }  // namespace
 
-#if DSE_WHEEL_HALF_TU
+#if DSE_WHEEL_PLAIN_TU
+// The full-geometry wheel kernel for ranges without bucketed primes (N up to
+// 1.1e12), on its own translation unit for its compile flags (Makefile).
+// wa: the caller's WheelArgs (the same definition, this source).
+hipError_t launch_wheel_plain(const void* table, const void* wa, uint32_t* out, unsigned long long* count,
+                              int num_cus, hipStream_t stream) {
+  return launch_wheel(table, *static_cast<const WheelArgs*>(wa), out, count, num_cus, stream);
+}
+#elif DSE_WHEEL_HALF_TU
 // The half-size geometry (this translation unit: 2^16 periods per segment):
 // the tail of a range whose last round of full segments would leave most
 // CUs idle (launch_sieve_range). Primes <= kWheelMaxPrime only.

@@ -5,7 +5,7 @@ NAME=$1; REV=$2; shift 2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 T=/tmp/dse_rev_$NAME
 rm -rf $T && mkdir -p $T/distributed-sieve-e_amd/csrc $T/include
-for f in dse_base.hip dse_wheel.hip dse_wheel_half.hip dse_host.cpp dse_internal.h Makefile; do
+for f in dse_base.hip dse_wheel.hip dse_wheel_half.hip dse_wheel_plain.hip dse_host.cpp dse_internal.h Makefile; do
   git -C $ROOT show $REV:distributed-sieve-e_amd/csrc/$f > $T/distributed-sieve-e_amd/csrc/$f 2>/dev/null || rm -f $T/distributed-sieve-e_amd/csrc/$f
 done
 git -C $ROOT show $REV:include/dse.h > $T/include/dse.h

@@ -11,6 +11,8 @@ $H -c -o /tmp/dse_var_$NAME/k.o $D/dse_base.hip
 W=${WHEEL_FLAGS-$(sed -n "s/^WHEEL_FLAGS ?= //p" $D/Makefile)}  # the Makefile's wheel flags unless set
 $H $W -c -o /tmp/dse_var_$NAME/w.o $D/dse_wheel.hip
 [ -f $D/dse_wheel_half.hip ] && $H $W -c -o /tmp/dse_var_$NAME/wh.o $D/dse_wheel_half.hip
+PL=${PLAIN_FLAGS-$(sed -n "s/^PLAIN_FLAGS ?= *//p" $D/Makefile)}
+[ -f $D/dse_wheel_plain.hip ] && $H $PL -c -o /tmp/dse_var_$NAME/wp.o $D/dse_wheel_plain.hip
 $H -c -o /tmp/dse_var_$NAME/h.o $D/dse_host.cpp
 $H -shared -o $OUT/libdse_$NAME.so /tmp/dse_var_$NAME/*.o -lrccl
 echo $OUT/libdse_$NAME.so
