@@ -11,3 +11,5 @@ timeout -k 10 300 python tools/config_sweep.py $O/configs_1gpu.json > $O/configs
 tail -8 $O/configs.log
 timeout -k 10 600 bash tools/profile.sh r03final || exit 1
 bash tools/gpu/window_kstats.sh
+timeout -k 10 420 python -u tools/parity_sweep.py 300 24301 > $O/parity_sweep.txt 2>&1 || { tail -5 $O/parity_sweep.txt; exit 1; }
+tail -1 $O/parity_sweep.txt
