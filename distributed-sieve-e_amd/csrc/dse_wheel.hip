@@ -1449,9 +1449,9 @@ constexpr uint32_t kBucketGrid1 = DSE_BK_GRID1;
 constexpr uint32_t kBucketCols = kBucketGrid1;
 static_assert(kBucketCols % 64 == 0, "column scan: whole lanes");
 #ifndef DSE_BK_SPLIT_LOG
-#define DSE_BK_SPLIT_LOG 26
+#define DSE_BK_SPLIT_LOG 28
 #endif
-constexpr uint32_t kBucketSplitLog = DSE_BK_SPLIT_LOG;  // production split: primes <= 2^26 one-level
+constexpr uint32_t kBucketSplitLog = DSE_BK_SPLIT_LOG;  // production split: primes <= 2^28 one-level
 constexpr uint32_t kBucketMaxSegs = DSE_BK_SEGS; // segments per pass (LDS counters)
 constexpr uint32_t kCoprime30 = (1u << 1) | (1u << 7) | (1u << 11) | (1u << 13) | (1u << 17) | (1u << 19) |
                                 (1u << 23) | (1u << 29);
@@ -1700,7 +1700,7 @@ __global__ __launch_bounds__(1024) void bucket_startscan_kernel(const uint32_t* 
 #define DSE_BK_CHUNK 32  // band-0 fill walks chunks of this many segments (0: prime by prime, A/B)
 #endif
 #ifndef DSE_BK_FILL_RG
-#define DSE_BK_FILL_RG 8
+#define DSE_BK_FILL_RG 16
 #endif
 constexpr uint32_t kFillRG = DSE_BK_FILL_RG;  // stride rounds of primes walked together (DSE_BK_CHUNK)
 
