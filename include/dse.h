@@ -184,7 +184,7 @@ int32_t dse_device_status(dse_ctx *ctx);
  *   (covers the multi-pass path on small windows); 0 = default.
  *   "bucket_split_log2" = k in 0..63: bucketed primes <= 2^k take the
  *   one-level fill, larger ones the two-level staged fill; 0 = the default
- *   split (2^25).
+ *   split (2^28).
  *   "wheel_geometry" = 0 (default): a range's last partial round of full
  *   segments is sieved as half-size segments when that is faster; 1: full
  *   segments only; 2: half-size segments only (covers that kernel in tests).
