@@ -808,7 +808,10 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
 constexpr uint32_t kBkBatchU = 16;                                // loads in flight per lane (bucket unit)
 constexpr uint32_t kBkUnit = 64 * kBkBatchU * DSE_BK_UNIT_BATCHES;  // band-1 entries per bucket unit
 constexpr uint32_t kBkGrid0 = DSE_BK_GRID;                         // band-0 columns (fill workgroups)
-constexpr uint32_t kBk0Lists = 16;                                 // band-0 columns per bucket unit
+#ifndef DSE_BK0_LISTS
+#define DSE_BK0_LISTS 16
+#endif
+constexpr uint32_t kBk0Lists = DSE_BK0_LISTS;                      // band-0 columns per bucket unit
 static_assert(kBkGrid0 % kBk0Lists == 0 && 64 % kBk0Lists == 0, "band-0 bucket units");
 
 struct WheelLds {
