@@ -1942,6 +1942,28 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_fill_stage_kernel(
     bucket_stage_wg(sm, x - nfill, table, ba, range, cols, start, tmp, nsup);
 }
 
+#ifndef DSE_BK_SPLIT_KERNELS
+#define DSE_BK_SPLIT_KERNELS 0  // 1: band-0 fill and band-1 stage as two kernels (own register allocations) (A/B)
+#endif
+// The two halves of bucket_fill_stage_kernel as kernels of their own: the
+// band-0 walk's round state (16 rounds in registers) does not then set the
+// stage's register allocation and occupancy.
+__global__ __launch_bounds__(kBucketThreads) void bucket_fill0_kernel(const void* __restrict__ table, BucketArgs ba,
+                                                                    const uint32_t* __restrict__ range, BandZero bz,
+                                                                    const uint32_t* __restrict__ flag) {
+  extern __shared__ uint32_t sm[];
+  if (flag[1]) return;
+  bucket_fill_wg(sm, blockIdx.x, table, ba, range, bz);
+}
+__global__ __launch_bounds__(kBucketThreads) void bucket_stage1_kernel(
+    const void* __restrict__ table, BucketArgs ba, const uint32_t* __restrict__ range,
+    const uint32_t* __restrict__ cols, const uint32_t* __restrict__ start, uint32_t* __restrict__ tmp,
+    uint32_t nsup, const uint32_t* __restrict__ flag) {
+  extern __shared__ uint32_t sm[];
+  if (flag[1]) return;
+  bucket_stage_wg(sm, blockIdx.x, table, ba, range, cols, start, tmp, nsup);
+}
+
 __global__ __launch_bounds__(kSortThreads) void bucket_sort_kernel(BucketArgs ba, const uint32_t* __restrict__ cols,
                                                                    const uint32_t* __restrict__ start,
                                                                    const uint32_t* __restrict__ tmp,
@@ -2355,8 +2377,28 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
         (e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bucket_fill_stage_kernel),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes)) != hipSuccess)
       return e;
+#if DSE_BK_SPLIT_KERNELS
+    {
+      const uint32_t l0 = 4 * (uint32_t)ns, l1 = 4 * stage_lds_words(nsup);
+      if (band1 && l1 > 65536 &&
+          (e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bucket_stage1_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)l1)) != hipSuccess)
+        return e;
+      if (band0 && l0 > 65536 &&
+          (e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bucket_fill0_kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)l0)) != hipSuccess)
+        return e;
+      if (band1)
+        hipLaunchKernelGGL(bucket_stage1_kernel, dim3(kBucketGrid1), dim3(kBucketThreads), l1, stream, table, ba,
+                           range, cols, start, tmp, nsup, scratch->flag);
+      if (band0)
+        hipLaunchKernelGGL(bucket_fill0_kernel, dim3(kBucketGrid), dim3(kBucketThreads), l0, stream, table, ba, range,
+                           bz, scratch->flag);
+    }
+#else
     hipLaunchKernelGGL(bucket_fill_stage_kernel, dim3(nfill + (band1 ? kBucketGrid1 : 0)), dim3(kBucketThreads),
                        lds_bytes, stream, table, ba, range, cols, start, bz, tmp, nsup, nfill, scratch->flag);
+#endif
     if (band1) {
       hipLaunchKernelGGL(bucket_sort_kernel, dim3(nsup * (kBucketGrid1 / kSortGroup)), dim3(kSortThreads), 0,
                          stream, ba, cols, start, tmp, ent, scratch->flag);
