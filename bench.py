@@ -164,7 +164,7 @@ def lds_instr_check(wm: int, cs: int, pmc):
     unit claims and the ds_or of predicated marks issued with part of the wave
     (A-class and B tails, L planes with <= 2 hits), which the analytic count
     of hits cannot see: ~2.3 K wave-instructions per segment at N=1e11
-    (DESIGN.md section 6), 11% of the total. A negative rest, or one far above
+    (DESIGN.md section 6), 9-11% of the total. A negative rest, or one far above
     that, would mean the analytic count is off. (A half-geometry tail segment
     has half the lane-rows and 51 instead of 95 init instructions per lane:
     counted here as full segments, < 0.1% at N=1e11.)"""
