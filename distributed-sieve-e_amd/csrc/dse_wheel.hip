@@ -2058,6 +2058,26 @@ __global__ __launch_bounds__(kSortThreads) void bucket_sort_kernel(BucketArgs ba
 #endif  // DSE_WHEEL_MAIN_TU
 }  // namespace
 
+#ifdef DSE_TIMING
+// profiling builds only: each wheel TU (main, plain, half) has its own g_timing;
+// read it, add it into acc and clear it
+#if DSE_WHEEL_PLAIN_TU
+int timing_take_plain(unsigned long long* acc) {
+#elif DSE_WHEEL_HALF_TU
+int timing_take_half(unsigned long long* acc) {
+#else
+int timing_take_plain(unsigned long long* acc);
+int timing_take_half(unsigned long long* acc);
+int timing_take_main(unsigned long long* acc) {
+#endif
+  unsigned long long t[8];
+  if (hipMemcpyFromSymbol(t, HIP_SYMBOL(g_timing), sizeof(t)) != hipSuccess) return -1;
+  for (int i = 0; i < 8; ++i) acc[i] += t[i];
+  const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_timing), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 #if DSE_WHEEL_MAIN_TU
 hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream, uint64_t n_hint) {
   const uint64_t grid = std::max<uint64_t>(4 * (uint64_t)num_cus, std::min<uint64_t>(n_hint / 1024 + 1, 1u << 16));
@@ -2066,11 +2086,10 @@ hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream, ui
 }
 
 #ifdef DSE_TIMING
-// profiling builds only: read and clear the per-phase cycle sums
+// profiling builds only: read and clear the per-phase cycle sums of all three wheel TUs
 extern "C" int dse_debug_timing(unsigned long long* out) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_timing), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
-  const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_timing), z, sizeof(z)) == hipSuccess ? 0 : -1;
+  for (int i = 0; i < 8; ++i) out[i] = 0;
+  return (timing_take_main(out) || timing_take_plain(out) || timing_take_half(out)) ? -1 : 0;
 }
 #endif
 
