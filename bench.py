@@ -142,8 +142,12 @@ def pmc_summary(N: int, P: int, window: bool):
                         steps.setdefault(r["Counter_Name"], set()).add(r["Dispatch_Id"])
             v = {k: x / len(steps[k]) for k, x in tot.items()}
             cyc = v["GRBM_GUI_ACTIVE"] / 8
+            try:
+                build = json.load(open(os.path.join(d, "pmc_build.json")))
+            except OSError:
+                build = None
             return {"traffic": (2 * v["FETCH_SIZE"] + v["WRITE_SIZE"]) * 1024, "source": os.path.relpath(d, ROOT),
-                    "cycles": cyc,
+                    "build": build, "cycles": cyc, "sq_insts_valu": v["SQ_INSTS_VALU"],
                     "valu_issue_per_cu_cycle": v["SQ_INSTS_VALU"] / work.NUM_CUS / cyc,
                     "valu_frac": v["SQ_INSTS_VALU"] / work.NUM_CUS / cyc / work.VALU_PEAK_PER_CU_CYCLE,
                     "lds_busy": v["SQ_LDS_IDX_ACTIVE"] / work.NUM_CUS / cyc,
@@ -215,6 +219,16 @@ def main():
         limit = S.base_limit_for_range(0, P * cs + tail_n)
         with_mask = not a.no_mask
     words = (cs + 63) // 64
+
+    # the world this run formed (a SCALE line shows its N ranks and their devices)
+    me = {"rank": rank, "local_rank": local, "device": torch.cuda.current_device(),
+          "pci_bus_id": getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", None)}
+    ranks = [me]
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+    world_info = {"backend": dist.get_backend() if world > 1 else None, "size": world, "ranks": ranks,
+                  "rehearsal": rehearse}
 
     ctx = S.Context(device=local)
     tbytes = S.base_table_bytes(limit)
@@ -327,10 +341,12 @@ def main():
             "verified": verified,
             "roofline": None,
             "cpu_baseline": None,
+            "world": world_info,
         }
         if rf is not None:
             wm = rf["wheel_marks"]
             achieved = work.LDS_OR_BYTES_PER_MARK * wm / ks / 1e9
+            mark_instr_per_cu = wm / 64 / work.NUM_CUS  # full-wave ds_or_b32 per CU
             out["roofline"] = {
                 "bound": "lds",
                 "achieved": achieved,
@@ -338,8 +354,16 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / work.LDS_OR_PEAK_GBS,
                 "traffic": pmc["traffic"] if pmc else None,
+                "traffic_source": f"committed PMC pass {pmc['source']} (not this run)" if pmc else None,
                 "basis": "executed ds_or_b32 marks (mod-30 wheel, primes > 61) x 4 B per kernel second against "
                          "the LDS store path (64 B/clk/CU); kernel time from HIP events on the launch stream",
+                "peak_ds_or": work.LDS_DS_OR_PEAK_GBS,
+                "frac_ds_or": achieved / work.LDS_DS_OR_PEAK_GBS,
+                "ds_or_basis": f"the measured conflict-free ds_or_b32 rate, {work.DS_OR_CYCLES_PER_WAVE_INSTR} "
+                               "CU-cycles per wave-instruction (profiles/r02/lds_conflict_microbench.txt)",
+                "cycles_per_mark_instr": ks * work.CLOCK_HZ / mark_instr_per_cu,
+                "cycles_per_mark_instr_basis": "live: kernel seconds x 2.4 GHz / (executed marks / 64 / 256 CUs); "
+                                               f"floor {work.DS_OR_CYCLES_PER_WAVE_INSTR}",
                 "kernel": "wheel_segments_kernel", "kernel_ms": ks * 1e3,
                 "executed_marks_per_launch": wm,
                 "frac_algorithmic": rf["frac"],
@@ -347,16 +371,27 @@ def main():
                 "algorithmic_basis": "SURVEY 8(d): 8 B x odd-only marks from p^2 / 78.6 TB/s; the wheel executes "
                                      f"{wm / rf['marks']:.3f} of them, so this exceeds 1",
                 "hbm_bytes_per_launch": rf["hbm_bytes"],
-                "hbm_frac": (pmc["traffic"] if pmc else rf["hbm_bytes"]) / ks / 1e9 / work.HBM_PEAK_GBS,
-                "valu_frac": pmc["valu_frac"] if pmc else None,
-                "valu_issue_per_cu_cycle": pmc["valu_issue_per_cu_cycle"] if pmc else None,
-                "lds_busy": pmc["lds_busy"] if pmc else None,
-                "lds_conflict_share": pmc["lds_conflict_share"] if pmc else None,
-                "pmc_source": pmc["source"] if pmc else None,
+                "hbm_frac_algorithmic": rf["hbm_bytes"] / ks / 1e9 / work.HBM_PEAK_GBS,
                 "executed_marks_source": "analytic (mail_sieve_e/work.py wheel_marks_for_range: multiples p*m >= p^2 "
                                          "with gcd(m, 30) = 1 of the primes 61 < p <= sqrt(N)), cross-checked "
-                                         "against SQ_INSTS_LDS in lds_instr_check",
-                "lds_instr_check": lds_instr_check(wm, cs, pmc),
+                                         "against SQ_INSTS_LDS in pmc_committed.lds_instr_check",
+                # Read from the newest committed rocprofv3 PMC passes of this config
+                # (profiles/<round>/pmc_*_sieve_kernel.csv), NOT measured in this run;
+                # `build` names the library those passes profiled.
+                "pmc_committed": None if not pmc else {
+                    "source": pmc["source"],
+                    "build": pmc["build"],
+                    "traffic": pmc["traffic"],
+                    "hbm_frac": pmc["traffic"] / ks / 1e9 / work.HBM_PEAK_GBS,
+                    "cycles_per_cu": pmc["cycles"],
+                    "cycles_per_mark_instr": pmc["cycles"] / mark_instr_per_cu,
+                    "valu_per_mark_instr": pmc["sq_insts_valu"] / (wm / 64),
+                    "valu_frac": pmc["valu_frac"],
+                    "valu_issue_per_cu_cycle": pmc["valu_issue_per_cu_cycle"],
+                    "lds_busy": pmc["lds_busy"],
+                    "lds_conflict_share": pmc["lds_conflict_share"],
+                    "lds_instr_check": lds_instr_check(wm, cs, pmc),
+                },
             }
         if world == 1 and a.cpu_baseline == "on" and not a.window:
             out["cpu_baseline"] = cpu_baseline(int(a.cpu_max_n))

@@ -181,7 +181,26 @@ __global__ __launch_bounds__(kBaseMaskThreads) void base_mask_kernel(uint64_t li
   }
 }
 
+// out[j] = sum over i < nsrc of in[i * n + j] (the logical-device stand-in for
+// the count all-reduce, dse_debug_init_logical)
+__global__ __launch_bounds__(256) void sum_rows_kernel(const unsigned long long* __restrict__ in, uint32_t nsrc,
+                                                       uint32_t n, unsigned long long* __restrict__ out) {
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
+    unsigned long long t = 0;
+    for (uint32_t i = 0; i < nsrc; ++i) t += in[(uint64_t)i * n + j];
+    out[j] = t;
+  }
+}
+
 }  // namespace
+
+hipError_t launch_sum_rows(const unsigned long long* in, uint32_t nsrc, uint32_t n, unsigned long long* out,
+                           hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(std::min<uint32_t>((n + 255) / 256, 1024u)), dim3(256), 0, stream, in,
+                     nsrc, n, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_base_primes(uint64_t limit, void* table, uint32_t cap, hipStream_t stream) {
   if (limit > kBaseLimitMax) return hipErrorInvalidValue;

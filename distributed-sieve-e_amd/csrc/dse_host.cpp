@@ -83,6 +83,7 @@ struct DevState {
   std::vector<hipStream_t> side;         // up to kSideStreams, created on first use
   std::vector<hipEvent_t> side_done;     // one per side stream
   hipEvent_t ready = nullptr;            // the table (and zeroed counts) on `stream`
+  hipEvent_t xev = nullptr;              // logical devices: this device's side of a collective
 };
 constexpr size_t kSideStreams = 4;       // the runtime's hardware queues per process (GPU_MAX_HW_QUEUES)
 
@@ -94,6 +95,13 @@ struct dse_ctx {
   int64_t last_n = -1;
   int32_t last_P = 0;
   dse::SieveOpts opts;  // test-only knobs (dse_debug_set_option)
+  // dse_debug_init_logical: every DevState on device 0, the collectives
+  // replaced by copies (xfer_table / allreduce_counts); on device 0:
+  bool logical = false;
+  unsigned long long* lg_stage = nullptr;  // gathered counts [devs][n]
+  unsigned long long* lg_sum = nullptr;    // their sum [n]
+  uint64_t lg_n = 0;                       // n of the two buffers
+  hipEvent_t lg_done = nullptr;            // the sum on device 0's stream
 };
 
 namespace {
@@ -133,9 +141,15 @@ int32_t build_table(DevState& d, uint64_t limit) {
 
 // Enqueue a copy of the sticky bucket-overflow flag on d.stream (before the
 // caller's stream sync); check_flag after the sync reports and clears it.
+// d.stream first waits for the last bucketed pass on the context's scratch,
+// whatever stream it ran on (an async pass on a user stream may still be
+// running: its overflow must neither be reported as this call's nor be
+// cleared before it is written).
 int32_t fetch_flag(DevState& d, uint32_t* h) {
   *h = 0;
-  if (d.scratch.flag) HIP_TRY(hipMemcpyAsync(h, d.scratch.flag, sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
+  if (!d.scratch.flag) return DSE_OK;
+  if (d.scratch.used) HIP_TRY(hipStreamWaitEvent(d.stream, d.scratch.done, 0));
+  HIP_TRY(hipMemcpyAsync(h, d.scratch.flag, sizeof(uint32_t), hipMemcpyDeviceToHost, d.stream));
   return DSE_OK;
 }
 
@@ -197,6 +211,17 @@ int32_t share_table(dse_ctx* ctx, uint64_t limit) {
   const int nd = (int)ctx->devs.size();
   if (nd == 1) return DSE_OK;
   const uint64_t pbytes = dse_base_table_prime_bytes(limit);
+  if (ctx->logical) {  // the broadcast as copies from device 0's table, each on its device's stream
+    DevState& r = ctx->devs[0];
+    HIP_TRY(hipEventRecord(r.xev, r.stream));
+    for (int i = 1; i < nd; ++i) {
+      DevState& d = ctx->devs[i];
+      HIP_TRY(hipStreamWaitEvent(d.stream, r.xev, 0));
+      HIP_TRY(hipMemcpyAsync(d.table, r.table, pbytes, hipMemcpyDeviceToDevice, d.stream));
+      HIP_TRY(dse::launch_wheel_offsets(d.table, d.num_cus, d.stream, prime_cap(limit)));
+    }
+    return DSE_OK;
+  }
   NCCL_TRY(ncclGroupStart());
   for (int i = 0; i < nd; ++i) {
     DevState& d = ctx->devs[i];
@@ -214,6 +239,38 @@ int32_t share_table(dse_ctx* ctx, uint64_t limit) {
 // Sum `n` uint64 counts over the devices with an RCCL all-reduce (in place).
 int32_t allreduce_counts(dse_ctx* ctx, uint64_t n) {
   if (ctx->devs.size() < 2) return DSE_OK;
+  if (ctx->logical) {  // gather + sum on device 0's stream, then every device copies the sum back
+    const uint32_t nd = (uint32_t)ctx->devs.size();
+    DevState& r = ctx->devs[0];
+    HIP_TRY(hipSetDevice(r.device));
+    if (ctx->lg_n < n) {
+      if (ctx->lg_stage) HIP_TRY(hipFree(ctx->lg_stage));
+      if (ctx->lg_sum) HIP_TRY(hipFree(ctx->lg_sum));
+      ctx->lg_stage = ctx->lg_sum = nullptr;
+      ctx->lg_n = 0;
+      HIP_TRY(hipMalloc(&ctx->lg_stage, nd * n * sizeof(unsigned long long)));
+      HIP_TRY(hipMalloc(&ctx->lg_sum, n * sizeof(unsigned long long)));
+      ctx->lg_n = n;
+    }
+    for (uint32_t i = 0; i < nd; ++i) {
+      DevState& d = ctx->devs[i];
+      if (i) {
+        HIP_TRY(hipEventRecord(d.xev, d.stream));
+        HIP_TRY(hipStreamWaitEvent(r.stream, d.xev, 0));
+      }
+      HIP_TRY(hipMemcpyAsync(ctx->lg_stage + i * n, d.counts, n * sizeof(unsigned long long),
+                             hipMemcpyDeviceToDevice, r.stream));
+    }
+    HIP_TRY(dse::launch_sum_rows(ctx->lg_stage, nd, (uint32_t)n, ctx->lg_sum, r.stream));
+    HIP_TRY(hipEventRecord(ctx->lg_done, r.stream));
+    for (uint32_t i = 0; i < nd; ++i) {
+      DevState& d = ctx->devs[i];
+      if (i) HIP_TRY(hipStreamWaitEvent(d.stream, ctx->lg_done, 0));
+      HIP_TRY(hipMemcpyAsync(d.counts, ctx->lg_sum, n * sizeof(unsigned long long), hipMemcpyDeviceToDevice,
+                             d.stream));
+    }
+    return DSE_OK;
+  }
   NCCL_TRY(ncclGroupStart());
   for (size_t i = 0; i < ctx->devs.size(); ++i) {
     DevState& d = ctx->devs[i];
@@ -240,6 +297,8 @@ int32_t dse_device_count(void) {
 }
 
 dse_ctx* dse_init(int32_t num_gpus) {
+  g_err.clear();
+  g_code = DSE_OK;
   int avail = 0;
   if (hipGetDeviceCount(&avail) != hipSuccess || avail < 1) {
     fail(DSE_EHIP, "no HIP device visible");
@@ -273,6 +332,8 @@ dse_ctx* dse_init(int32_t num_gpus) {
 }
 
 dse_ctx* dse_init_device(int32_t device) {
+  g_err.clear();
+  g_code = DSE_OK;
   int avail = 0;
   if (hipGetDeviceCount(&avail) != hipSuccess || device < 0 || device >= avail) {
     fail(DSE_EINVAL, "device " + std::to_string(device) + " not visible");
@@ -290,6 +351,12 @@ dse_ctx* dse_init_device(int32_t device) {
 void dse_destroy(dse_ctx* ctx) {
   if (!ctx) return;
   for (auto& c : ctx->comms) ncclCommDestroy(c);
+  if (ctx->logical && !ctx->devs.empty()) {
+    (void)hipSetDevice(ctx->devs[0].device);
+    if (ctx->lg_stage) (void)hipFree(ctx->lg_stage);
+    if (ctx->lg_sum) (void)hipFree(ctx->lg_sum);
+    if (ctx->lg_done) (void)hipEventDestroy(ctx->lg_done);
+  }
   for (auto& d : ctx->devs) {
     (void)hipSetDevice(d.device);
     free_resident(d);
@@ -300,9 +367,41 @@ void dse_destroy(dse_ctx* ctx) {
     for (auto st : d.side) (void)hipStreamDestroy(st);
     for (auto ev : d.side_done) (void)hipEventDestroy(ev);
     if (d.ready) (void)hipEventDestroy(d.ready);
+    if (d.xev) (void)hipEventDestroy(d.xev);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
   delete ctx;
+}
+
+dse_ctx* dse_debug_init_logical(int32_t num_logical) {
+  g_err.clear();
+  g_code = DSE_OK;
+  int avail = 0;
+  if (hipGetDeviceCount(&avail) != hipSuccess || avail < 1) {
+    fail(DSE_EHIP, "no HIP device visible");
+    return nullptr;
+  }
+  if (num_logical < 1 || num_logical > 64) {
+    fail(DSE_EINVAL, "num_logical must be in 1..64");
+    return nullptr;
+  }
+  dse_ctx* ctx = new dse_ctx();
+  ctx->logical = true;
+  ctx->devs.resize(num_logical);
+  for (int i = 0; i < num_logical; ++i) {
+    DevState& d = ctx->devs[i];
+    if (init_dev(d, 0) != DSE_OK || hipEventCreateWithFlags(&d.xev, hipEventDisableTiming) != hipSuccess) {
+      if (!g_code) fail(DSE_EHIP, "event creation failed");
+      dse_destroy(ctx);
+      return nullptr;
+    }
+  }
+  if (hipEventCreateWithFlags(&ctx->lg_done, hipEventDisableTiming) != hipSuccess) {
+    fail(DSE_EHIP, "event creation failed");
+    dse_destroy(ctx);
+    return nullptr;
+  }
+  return ctx;
 }
 
 int32_t dse_ctx_num_devices(const dse_ctx* ctx) { return ctx ? (int32_t)ctx->devs.size() : 0; }
@@ -625,6 +724,11 @@ int32_t dse_debug_set_option(dse_ctx* ctx, const char* name, int64_t value) {
   if (n == "bucket_k0_divisor") {
     if (value < 0 || value > 0xFFFFFFFFll) return fail(DSE_EINVAL, "bucket_k0_divisor out of range");
     ctx->opts.bucket_k0_div = (uint32_t)value;
+    return DSE_OK;
+  }
+  if (n == "scratch_poison") {
+    if (value < 0 || value > 1) return fail(DSE_EINVAL, "scratch_poison must be 0 or 1");
+    ctx->opts.scratch_poison = (uint32_t)value;
     return DSE_OK;
   }
   if (n == "bucket_cap_divisor") {

@@ -35,8 +35,8 @@ constexpr uint32_t kR30[8] = {1, 7, 11, 13, 17, 19, 23, 29};
 
 // Mod-30 wheel segment geometry (dse_wheel.hip): a segment is 2^17 periods of
 // 30 integers, 8 planes (one per coprime residue) x 8 columns of 2^14 periods
-// (one 128 KiB LDS image). The two-image pipelined variant
-// (-DDSE_PIPELINE=1 -DDSE_WHEEL_LOG_KP=16) halves it.
+// (one 128 KiB LDS image). dse_wheel_half.hip compiles the same kernel with
+// 2^16 periods per segment (range tails).
 #ifndef DSE_WHEEL_LOG_KP
 #define DSE_WHEEL_LOG_KP 17
 #endif
@@ -77,9 +77,13 @@ struct SieveOpts {
   uint32_t bucket_cap_div = 0;    // > 1: divide the (rigorous) bucket entry capacities, to test the overflow flag
   uint32_t bucket_k0_div = 0;     // > 1: divide the band-0 region capacity, to test the spill list
   uint32_t wheel_geometry = 0;    // ranges without buckets: 0 auto (half-size tail), 1 full only, 2 half only
+  uint32_t scratch_poison = 0;    // 1: fill the bucket scratch with 0xFF bytes before every pass (stale contents)
 };
 
 hipError_t launch_base_primes(uint64_t limit, void* table, uint32_t cap, hipStream_t stream);
+// out[j] = sum_i in[i * n + j], i < nsrc (dse_debug_init_logical's count all-reduce)
+hipError_t launch_sum_rows(const unsigned long long* in, uint32_t nsrc, uint32_t n, unsigned long long* out,
+                           hipStream_t stream);
 // Any limit <= kBigBaseLimitMax: the multi-workgroup kernel up to kBaseLimitMax,
 // above it a sieve of [3, limit] by the wheel kernel + ordered compaction.
 hipError_t launch_base_primes_big(uint64_t limit, void* table, uint32_t cap, int num_cus, hipStream_t stream);

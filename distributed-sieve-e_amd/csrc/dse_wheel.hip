@@ -36,8 +36,6 @@
 //      the small primes 3..61, masks the range end, popcounts, stores; then
 //      each wave inits (patterns of 7..61) the rows it expanded, for the next
 //      segment.
-// DSE_PIPELINE=1 (variant, slower: DESIGN.md section 4.1) uses two 64 KiB
-// images: expander waves expand/init one while the others mark the other.
 // See DESIGN.md section 4 for the rooflines.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -53,35 +51,16 @@
 namespace dse {
 namespace {
 
-constexpr uint32_t kPhaseMidA = 1, kPhaseMidB = 2, kPhaseLarge = 4, kPhaseSmall = 8, kPhaseStore = 16,
-                   kPhaseExpand = 32, kPhaseUnits = 64;
-constexpr uint32_t kPhaseAll = 127;
-
 constexpr uint32_t KP = 1u << kWheelLogKP;  // periods per segment (per plane)
 constexpr uint32_t LOG_LS = kWheelLogKP - 3;
 constexpr uint32_t LS = 1u << LOG_LS;       // periods per column
 constexpr uint32_t ROWS = LS / 32;          // words per column
 constexpr uint32_t IMG_WORDS = 64 * ROWS;   // one segment image
 constexpr uint32_t NT = 1024;
-constexpr uint32_t NW = NT / 64;
-#ifndef DSE_PIPELINE
-#define DSE_PIPELINE 0
-#endif
-#ifndef DSE_NE
-#define DSE_NE (DSE_PIPELINE ? 8 : 16)
-#endif
-constexpr uint32_t NIMG = DSE_PIPELINE ? 2 : 1;  // segment images in LDS
-constexpr uint32_t NE = DSE_NE;             // waves that expand and init
-static_assert(NE >= 1 && NE <= NW && (DSE_PIPELINE ? NE < NW : NE == NW) && ROWS % (8 * NE) == 0,
-              "expander rows");
+constexpr uint32_t NW = NT / 64;            // waves; every wave marks, expands and inits
+static_assert(ROWS % (8 * NW) == 0, "expander rows");
 #ifndef DSE_TA
 #define DSE_TA 256
-#endif
-#ifndef DSE_L_SETS
-#define DSE_L_SETS 2  // sets of 64 primes per L unit (A/B)
-#endif
-#ifndef DSE_B_PRED_EXEC
-#define DSE_B_PRED_EXEC 1  // 0: predicated-off A-class and B-tail marks OR 0 inside the image (A/B)
 #endif
 #ifndef DSE_WHEEL_HALF_TU
 #define DSE_WHEEL_HALF_TU 0  // 1: compiled by dse_wheel_half.hip with 2^16 periods per segment
@@ -105,29 +84,13 @@ static_assert(TB <= LS && TB >= TA, "B/L threshold");
 constexpr uint32_t kMidCap = TB >= 16384 ? 1920 : TB >= 8192 ? 1040 : TB >= 4096 ? 580 : 320;  // odd primes in (61, TB]
 constexpr uint32_t kOutWordsPerSeg = (uint32_t)(kWheelOutBits / 32);  // 30720
 
-constexpr int kNQ = 15;
-constexpr uint32_t kQ[kNQ] = {7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61};
-constexpr uint32_t kQMax = 61;
+constexpr uint32_t kQMax = 61;  // the pattern primes are 7..61
 
-constexpr uint64_t pat64(uint32_t q) {
-  uint64_t v = 0;
-  for (uint32_t k = 0; k < 64; k += q) v |= 1ull << k;
-  return v;
-}
 constexpr uint32_t inv30_const(uint32_t q) {
   for (uint32_t x = 1; x < q; ++x)
     if ((30 * x) % q == 1) return x;
   return 0;
 }
-// 30^{-1} mod q of the pattern primes, as constant tables: called in device
-// code outside a constant expression, inv30_const is not folded and runs its
-// search loop on the scalar unit at every call (it made the first init-table
-// builds 3.4x slower).
-constexpr uint32_t kQInv30[kNQ] = {inv30_const(7),  inv30_const(11), inv30_const(13), inv30_const(17),
-                                   inv30_const(19), inv30_const(23), inv30_const(29), inv30_const(31),
-                                   inv30_const(37), inv30_const(41), inv30_const(43), inv30_const(47),
-                                   inv30_const(53), inv30_const(59), inv30_const(61)};
-
 // Init tables: the 15 small primes in 7 groups G with period M_G = prod(G).
 // U_G[y] = 1 iff some q in G divides y. Plane i period k holds the value
 // Vs + rho_i + 30k, and q | Vs + rho_i + 30k <=> q | k + c_G with
@@ -137,33 +100,17 @@ constexpr uint32_t kQInv30[kNQ] = {inv30_const(7),  inv30_const(11), inv30_const
 // offset o, read as 9 aligned ds_read_b128 from the copy of the string that
 // is shifted by (o >> 5) & 3 dwords (4 copies), so every read is aligned
 // whatever o is; word r = alignbit(U[d0 + r + 1], U[d0 + r], o & 31).
-// DSE_INIT_REGS=1 keeps the round-1 register-shift init (A/B).
-#ifndef DSE_INIT_REGS
-#define DSE_INIT_REGS 0
-#endif
-#ifndef DSE_PRIO
-#define DSE_PRIO 0  // 1: s_setprio(wave / 4) over expand + init; 2: for the whole kernel (A/B)
-#endif
-#ifndef DSE_BK_NO_M
-#define DSE_BK_NO_M 1  // 0: bucket walks read m[] (Barrett factors of every table prime) (A/B)
-#endif
 #ifndef DSE_BK_GRID
 #define DSE_BK_GRID 1024  // band-0 fill workgroups (columns)
 #endif
 #ifndef DSE_BK_UNIT_BATCHES
 #define DSE_BK_UNIT_BATCHES 4
 #endif
-#ifndef DSE_LUT_GLOBAL
-#define DSE_LUT_GLOBAL 0  // 1: expansion table read from global memory (L1) instead of LDS (A/B)
-#endif
-#ifndef DSE_INIT_GLOBAL
-#define DSE_INIT_GLOBAL 0  // 1: init tables read from global memory (L1) instead of LDS (A/B)
-#endif
 constexpr int kNG = 7;
 constexpr uint32_t kGQ[kNG][3] = {{7, 11, 13}, {17, 19, 1}, {23, 29, 1}, {31, 37, 1},
                                   {41, 43, 1}, {47, 53, 1}, {59, 61, 1}};
 constexpr uint32_t gmod(int g) { return kGQ[g][0] * kGQ[g][1] * kGQ[g][2]; }
-constexpr uint32_t kInitRun = 32 * (ROWS / NE);  // periods one lane inits per segment (one column)
+constexpr uint32_t kInitRun = 32 * (ROWS / NW);  // periods one lane inits per segment (one column)
 constexpr uint32_t kInitBlocks = kInitRun / 128 + 1;  // ds_read_b128 per lane and group
 // dwords per group string and copy: the reads reach dword d0 + 4 kInitBlocks - 1, d0 < M_G/32 + 1
 constexpr uint32_t gdw(int g) { return ((gmod(g) + 32 * (4 * kInitBlocks + 1) + 127) / 128) * 4; }
@@ -173,7 +120,6 @@ constexpr uint32_t kGInv30[kNG] = {inv30_const(gmod(0)), inv30_const(gmod(1)), i
                                    inv30_const(gmod(3)), inv30_const(gmod(4)), inv30_const(gmod(5)),
                                    inv30_const(gmod(6))};
 
-#if !DSE_INIT_REGS
 // The init tables, built at compile time (a launch copies them into LDS):
 // copy k, group g, dword gbase(g) + j = bits [32 (j + k), 32 (j + k) + 32) of U_g.
 struct InitTables {
@@ -196,34 +142,6 @@ constexpr InitTables make_init_tables() {
   return t;
 }
 __device__ const InitTables g_init_tables = make_init_tables();
-#endif
-
-#if DSE_LUT_GLOBAL
-// The expansion table for each of the 15 values of V0 mod 30 (V0 even): entry
-// v ^ 3 (v >> 5) = the prime odd slots of a period whose plane composite bits
-// are v (as the LDS table the kernel builds per launch).
-struct ExpandLuts {
-  uint32_t w[15 * 256];
-};
-constexpr ExpandLuts make_expand_luts() {
-  ExpandLuts t{};
-  for (uint32_t m = 0; m < 15; ++m) {
-    uint32_t rho[8] = {}, n = 0;
-    for (uint32_t r = 1; r < 30; r += 2) {
-      const uint32_t x = (2 * m + r) % 30;
-      if (x % 3 != 0 && x % 5 != 0) rho[n++] = r;
-    }
-    for (uint32_t v = 0; v < 256; ++v) {
-      uint32_t e = 0;
-      for (uint32_t i = 0; i < 8; ++i)
-        if (!(v & (1u << i))) e |= 1u << ((rho[i] - 1) >> 1);
-      t.w[256 * m + (DSE_LUT_GLOBAL == 2 ? v : v ^ (3u * (v >> 5)))] = e;
-    }
-  }
-  return t;
-}
-__device__ const ExpandLuts g_expand_luts = make_expand_luts();
-#endif
 
 struct WheelArgs {
   uint64_t V0;         // v_start - 1
@@ -233,8 +151,6 @@ struct WheelArgs {
   uint32_t pl_pack;    // plane of absolute residue R30[j] in bits [3j, 3j+3)
   uint32_t e_iota;     // bit j: floor((V0 + rho)/30) = KB0 + 1 for the plane of R30[j]
   uint32_t fix0;       // output word 0 bits of the primes 3..61 inside the range
-  uint32_t phases;
-  uint8_t v0q[kNQ];    // V0 mod q
   uint16_t v0g[kNG];   // V0 mod M_G (init tables)
   uint32_t nthr[4];    // odd primes <= 61, <= TA, <= TB, <= kWheelMaxPrime (table indices of the unit lists)
   // Bucketed hits of the primes > kWheelMaxPrime (bk_start null: none), as
@@ -248,10 +164,6 @@ struct WheelArgs {
   uint64_t bk_spill_cap;               //   (at most this many stored)
   uint32_t bk_k0;              // band-0 region capacity (0: no band 0 in the pass)
 };
-
-__device__ __forceinline__ void lds_or(uint32_t* a, uint32_t v) {
-  __hip_atomic_fetch_or(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
 
 // 32-bit LDS byte address of a __shared__ pointer.
 __device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
@@ -328,21 +240,8 @@ __device__ __forceinline__ uint32_t mark_run(uint32_t cb, uint32_t off, uint32_t
 // offset of the next hit. A lane without the hit leaves the ds_or (exec mask:
 // no bit select, and idle lanes take no part in bank conflicts).
 __device__ __forceinline__ uint32_t mark_col_pred(uint32_t cb, uint32_t off, uint32_t p, uint32_t one) {
-#if DSE_B_PRED_EXEC
   if (off < LS) mark_col_step(cb, off, p, one);
   return off;
-#endif
-  const bool hit = off < LS;
-  const uint32_t bit = hit ? shl1(off, one) : 0u;
-  uint32_t a;
-  asm volatile(
-      "v_lshlrev_b32 %0, 3, %1\n\t"
-      "v_and_or_b32 %0, %0, %3, %2\n\t"
-      "ds_or_b32 %0, %4"
-      : "=&v"(a)
-      : "v"(off), "v"(cb), "s"((ROWS - 1) << 8), "v"(bit)
-      : "memory");
-  return hit ? off + p : off;
 }
 
 // x mod p for x < 2^63 with m = floor((2^64-1)/p).
@@ -492,9 +391,8 @@ __device__ __forceinline__ void mark_at(uint32_t a, uint32_t bit) {
 // and sit p rows apart, so after 4 VALU of class setup each further mark is
 // one v_add of the wave-uniform 256 p (instead of 4 VALU per mark). Every
 // class has K = ROWS / p or K + 1 hits (its first row is < p): K marks, then
-// one predicated by row < ROWS, whose address is folded back into the image
-// (an OR of 0 there). off = first hit in the column (< p), img0 = image base
-// (aligned to the image size).
+// one predicated by row < ROWS (exec mask). off = first hit in the column
+// (< p), img0 = image base (aligned to the image size).
 #ifndef DSE_TA_CLS
 #define DSE_TA_CLS 224
 #endif
@@ -518,12 +416,7 @@ __device__ __forceinline__ void a_classes(uint32_t img0, uint32_t cb_col, uint32
       mark_at(a, bit);
       a += D;
     }
-    const bool in = a < img0 + IMG_BYTES;
-#if DSE_B_PRED_EXEC
-    if (in) mark_at(a, bit);  // exec mask, as mark_col_pred
-#else
-    mark_at((a & (IMG_BYTES - 1)) | img0, in ? bit : 0u);
-#endif
+    if (a < img0 + IMG_BYTES) mark_at(a, bit);  // exec mask, as mark_col_pred
     off = opaque(off + p);
   }
 }
@@ -630,28 +523,17 @@ __device__ __forceinline__ void load_L(LargeOps& o, const uint32_t* __restrict__
 }
 
 // Mark plane-relative period kk of plane byte base pb4 = image + 4 * plane:
-// word (row (kk >> 5) & (ROWS-1), column 8 * ((kk >> LOG_LS) & 7) + plane).
-// The masks keep any kk inside the image, so a predicated-off mark (PRED and
-// kk >= KP) is an OR of 0 at a valid address. asm for the same reason as
-// mark_col.
-#ifndef DSE_PRED_EXEC
-#define DSE_PRED_EXEC 1  // 0: predicated-off marks OR 0 instead of leaving the instruction (exec mask) (A/B)
-#endif
+// word (row (kk >> 5) & (ROWS-1), column 8 * (kk >> LOG_LS) + plane). PRED:
+// only if kk < KP -- a lane without a hit leaves the ds_or (exec mask), so it
+// adds no bank conflict (an OR of 0 at a random column conflicts like a
+// mark). asm for the same reason as mark_col.
 template <bool PRED>
 __device__ __forceinline__ void mark_plane(uint32_t pb4, uint32_t kk, uint32_t one) {
-#if DSE_PRED_EXEC
-  // a lane without a hit takes no part in the ds_or, so it adds no bank
-  // conflict (an OR of 0 at a random column conflicts like a mark)
   if (PRED && kk >= KP) return;
-  constexpr bool kOr0 = false;
-#else
-  constexpr bool kOr0 = PRED;
-#endif
   // kk < KP wherever the mark is executed: the column is kk >> LOG_LS (a
   // 4-byte shift, not an 8-byte bfe)
-  const uint32_t col = kOr0 ? __builtin_amdgcn_ubfe(kk, LOG_LS, 3) : kk >> LOG_LS;
-  uint32_t bit = shl1(kk, one);
-  if (kOr0) bit = kk < KP ? bit : 0u;
+  const uint32_t col = kk >> LOG_LS;
+  const uint32_t bit = shl1(kk, one);
   uint32_t a, t;
   asm volatile(
       "v_lshl_or_b32 %1, %2, 5, %3\n\t"
@@ -691,13 +573,9 @@ struct PlaneSteps {
   uint32_t one;  // 1 in a VGPR (shl1)
 };
 
-#ifndef DSE_L_ADD3
-#define DSE_L_ADD3 1  // 0: plane starts as the compiler's add/sub/add/min (4 VALU) (A/B)
-#endif
 // Plane start (a - Kb - e) mod p = min(t, t + p), t = a + (-Kb mod p) + (-e)
 // as one v_add3 (left to itself the compiler forms a - (kbm + e): 4 VALU).
 __device__ __forceinline__ uint32_t plane_start(uint32_t a, uint32_t nKbm, uint32_t ne, uint32_t p) {
-#if DSE_L_ADD3
   uint32_t t, u;
   asm("v_add3_u32 %0, %2, %3, %4\n\t"
       "v_add_u32 %1, %0, %5\n\t"
@@ -705,10 +583,6 @@ __device__ __forceinline__ uint32_t plane_start(uint32_t a, uint32_t nKbm, uint3
       : "=&v"(t), "=&v"(u)
       : "v"(a), "v"(nKbm), "v"(ne), "v"(p));
   return t;
-#else
-  const uint32_t t = a + nKbm + ne;
-  return min(t, t + p);
-#endif
 }
 
 // Branch-free body of an L unit whose 64 primes are all live and past p^2
@@ -778,8 +652,7 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
   }
   const uint32_t D = slow && live ? (uint32_t)(p2 - Vs) : 0u;
   if (!live) return;
-  // Primes above KP/2 mark branch-free: a predicated-off mark is an OR of 0 at
-  // an address inside the image (mark_plane<true>).
+  // Primes above KP/2 mark branch-free: two predicated marks (mark_plane<true>).
 #pragma unroll
   for (uint32_t q = 0; q < 8; ++q) {
     uint32_t kk = plane_start(o.a[q], nKbm, ps.ne[q], p);
@@ -815,23 +688,15 @@ constexpr uint32_t kBk0Lists = DSE_BK0_LISTS;                      // band-0 col
 static_assert(kBkGrid0 % kBk0Lists == 0 && 64 % kBk0Lists == 0, "band-0 bucket units");
 
 struct WheelLds {
-  uint32_t img[NIMG][IMG_WORDS];   // the segment image(s), at LDS address 0
+  uint32_t img[IMG_WORDS];         // the segment image, at LDS address 0
   uint64_t mid_m[kMidCap];         // Barrett factors of the staged mid primes
   uint32_t mid_p[kMidCap];         // p | (30^{-1} mod p) << 16
   uint32_t lut[256];               // period byte -> 15 odd slots
-#if !DSE_INIT_REGS
-#if !DSE_INIT_GLOBAL
   uint4 itab[kGDW];                // init tables U_G, 4 copies shifted by 0..3 dwords (kGDW / 4 blocks each)
-#endif
-#endif
   uint32_t thr[4];
-  uint32_t ctr[2];                 // unit counters (pipelined: one per image)
+  uint32_t ctr;                    // unit counter
   unsigned long long wave_cnt[NW];
 };
-
-#ifdef DSE_TIMING
-__device__ unsigned long long g_timing[8];
-#endif
 
 // BK: the range has bucketed primes (wa.bk_*). Two instantiations, so the
 // ranges without (N up to 1.1e12) run a unit loop without the bucket code
@@ -857,28 +722,6 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + table_a_offset(th->cap));
 
   const uint32_t tid = threadIdx.x, lane_id = tid & 63, wave = tid >> 6;
-#ifdef DSE_TIMING
-  // profiling builds (tools/build_variant.sh timing -DDSE_TIMING): per-wave
-  // cycles of mark / mark barrier / expand / init / segment barrier, summed
-  // over segments and waves into g_timing (dse_debug_timing)
-  uint64_t t_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t_prev = 0;  // + A, B, L unit time (drained)
-#define DSE_TSTAMP(i)                                              \
-  do {                                                             \
-    const uint64_t t_now = __builtin_amdgcn_s_memtime();           \
-    if ((i) > 0) t_acc[(i) - 1] += t_now - t_prev;                 \
-    t_prev = t_now;                                                \
-  } while (0)
-#else
-#define DSE_TSTAMP(i) \
-  do {                \
-  } while (0)
-#endif
-  const bool expander = wave < NE;
-#ifdef DSE_PHASE_KNOB
-  const uint32_t phases = wa.phases;  // ablation builds (tools/build_variant.sh knob -DDSE_PHASE_KNOB)
-#else
-  constexpr uint32_t phases = kPhaseAll;  // a runtime mask costs SGPRs (spill reloads in the unit loop)
-#endif
 
   if (tid == 0) {
     // first index with p > 61, with p > TA, with p > TB (capped by the LDS
@@ -889,8 +732,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     s_thr[1] = min(wa.nthr[1], np);
     s_thr[2] = min(min(wa.nthr[2], np), s_thr[0] + kMidCap);
     s_thr[3] = max(s_thr[2], min(wa.nthr[3], np));
-    lds.ctr[0] = 0;
-    lds.ctr[1] = 0;
+    lds.ctr = 0;
   }
   if (tid < 256) {
     uint32_t v = 0;
@@ -903,11 +745,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     // under lut_index(tid) (see there)
     s_lut[tid ^ (3u * (tid >> 5))] = v;
   }
-#if !DSE_INIT_REGS
-#if !DSE_INIT_GLOBAL
   for (uint32_t idx = tid; idx < 4 * kGDW; idx += NT) reinterpret_cast<uint32_t*>(lds.itab)[idx] = g_init_tables.w[idx];
-#endif
-#endif
   __syncthreads();
   const uint32_t i_mid0 = s_thr[0], i_midB = s_thr[1], i_mid1 = s_thr[2];
   for (uint32_t i = tid; i < i_mid1 - i_mid0; i += NT) {
@@ -916,15 +754,15 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     s_mid_m[i] = M[i_mid0 + i];
   }
   // Work units: list 1 = nA single mid primes, then nB diagonal units (8
-  // primes each); list 2 = nL large units (64 primes each); handed out through
-  // one dynamic queue per image. Issue arbitration favours older waves, so
+  // primes each); list 2 = nL large units (two sets of 64 primes each); handed
+  // out through one dynamic queue. Issue arbitration favours older waves, so
   // any static split finishes the youngest waves last; the queue makes them
-  // take fewer units instead, and lets the expanders join when done.
+  // take fewer units instead.
   const uint32_t nA = i_midB - i_mid0;
   const uint32_t n_mid = i_mid1 - i_mid0;
   const uint32_t nB = (i_mid1 - i_midB + 7) / 8;
   const uint32_t i_big = s_thr[3];             // L units end here
-  constexpr uint32_t kLU = 64 * DSE_L_SETS;  // primes per L unit
+  constexpr uint32_t kLU = 128;                // primes per L unit
   const uint32_t nL = (i_big - i_mid1 + kLU - 1) / kLU;
   const uint32_t n1 = nA + nB, n2 = nL;
 
@@ -934,50 +772,17 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   const uint32_t T = blockIdx.x < nseg ? (uint32_t)((nseg - 1 - blockIdx.x) / grid + 1) : 0u;  // rounds
   unsigned long long my_count = 0;
 
-  // ---- init: small-prime patterns (7..61) of segment s into an image.
-  // Expander wave w writes rows w*ROWS/NE .. +ROWS/NE of every column: the
-  // rows it expands, so it may init an image right after expanding it.
+  // ---- init: small-prime patterns (7..61) of segment s into the image.
+  // Wave w writes rows w*ROWS/NW .. +ROWS/NW of every column: the rows it
+  // expands, so it may init the image right after expanding it.
   auto init_segment = [&](uint32_t* __restrict__ img, uint64_t s) {
     uint32_t lane = lane_id;
     asm volatile("" : "+v"(lane));
     const uint32_t C = lane, pl = lane & 7, c = lane >> 3;
     const uint32_t rho = (uint32_t)(wa.rho_pack >> (5 * pl)) & 31u;
-    const uint32_t r0 = wave * (ROWS / NE);
+    const uint32_t r0 = wave * (ROWS / NW);
     const uint32_t k0 = c * LS + 32 * r0;                // first period of the lane's words
-    const bool on = phases & kPhaseSmall;
-#ifdef DSE_PHASE_KNOB
-    if (!on) {  // ablation: zero-fill only, no pattern arithmetic
-      for (uint32_t r = 0; r < ROWS / NE; ++r) img[(r0 + r) * 64 + C] = 0;
-      return;
-    }
-#endif
-#if DSE_INIT_REGS
-    uint32_t res[kNQ];
-#pragma unroll
-    for (int j = 0; j < kNQ; ++j) {
-      const uint32_t q = kQ[j];
-      // (Vs + rho + 30 k0) mod q, Vs = V0 + s*W
-      const uint32_t wq = (uint32_t)(kWheelSpan % q);
-      const uint32_t sq = (uint32_t)(s % q);
-      const uint32_t x = ((uint32_t)wa.v0q[j] + sq * wq + rho + (30u * k0) % q) % q;
-      const uint32_t u = x ? q - x : 0u;
-      res[j] = (u * kQInv30[j]) % q;                     // first k >= k0 with q | value, minus k0
-    }
-#pragma unroll 2
-    for (uint32_t r = 0; r < ROWS / NE; r += 2) {
-      uint64_t w = 0;
-#pragma unroll
-      for (int j = 0; j < kNQ; ++j) {
-        const uint32_t q = kQ[j];
-        const uint32_t d = 64 % q;
-        w |= pat64(q) << res[j];
-        res[j] = res[j] >= d ? res[j] - d : res[j] + q - d;
-      }
-      img[(r0 + r) * 64 + C] = (uint32_t)w;
-      img[(r0 + r + 1) * 64 + C] = (uint32_t)(w >> 32);
-    }
-#else
-    constexpr uint32_t R = ROWS / NE;  // words per lane
+    constexpr uint32_t R = ROWS / NW;  // words per lane
     constexpr uint32_t H = 16;         // words per pass (bounds the registers: 16 acc + 20 read)
     static_assert(R % H == 0 && H % 4 == 0, "init passes");
     uint32_t boff[kNG], bsh[kNG];      // per group: the lane's first aligned 16-byte block, bit shift
@@ -1003,13 +808,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       for (uint32_t r = 0; r < H; ++r) acc[r] = 0;
 #pragma unroll
       for (int g = 0; g < kNG; ++g) {
-#if DSE_INIT_GLOBAL
-        // from the vector L1 (a 10 KB table every CU reads): the reads leave
-        // the LDS to the expansion running beside them
-        const uint4* bp = reinterpret_cast<const uint4*>(g_init_tables.w) + boff[g] + h / 4;
-#else
         const uint4* bp = lds.itab + boff[g] + h / 4;
-#endif
         uint32_t blk[H + 4];
 #pragma unroll
         for (uint32_t b = 0; b < H / 4 + 1; ++b) {
@@ -1023,13 +822,12 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
 #pragma unroll
       for (uint32_t r = 0; r < H; ++r) img[(r0 + h + r) * 64 + C] = acc[r];
     }
-#endif
   };
 
   // ---- expand segment s (image img) to odd-only bits, count, store: lane
-  // (column c, row) of expander wave w reads that row of column c in all 8
-  // planes (32 contiguous bytes, two ds_read_b128), rows
-  // 8 * (ROWS/(8 NE) * w + t) + ro. ds_read_b128 serves a wave in 4 lane
+  // (column c, row) of wave w reads that row of column c in all 8 planes (32
+  // contiguous bytes, two ds_read_b128), rows
+  // 8 * (ROWS/(8 NW) * w + t) + ro. ds_read_b128 serves a wave in 4 lane
   // groups of 16 ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same + 32,
   // MI355X_MICROARCH.md section LDS); lane k of group g takes row offset
   // ro = 2g + (k & 1) and column c = k >> 1, and odd rows read their upper 16
@@ -1043,12 +841,9 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     const uint32_t ro = 2 * (2 * (lane >> 5) + gsub) + (k & 1), c = k >> 1;
     const bool odd = k & 1;
     const uint64_t seg_word0 = s * (uint64_t)kOutWordsPerSeg;
-#if DSE_LUT_GLOBAL
-    const uint32_t* __restrict__ g_lut = g_expand_luts.w + 256 * (uint32_t)((wa.V0 % 30) / 2);
-#endif
 #pragma unroll 1
-    for (uint32_t t = 0; t < ROWS / (NE * 8); ++t) {
-      const uint32_t row = 8 * ((ROWS / (NE * 8)) * wave + t) + ro;
+    for (uint32_t t = 0; t < ROWS / (NW * 8); ++t) {
+      const uint32_t row = 8 * ((ROWS / (NW * 8)) * wave + t) + ro;
       const uint4* rp = reinterpret_cast<const uint4*>(img + row * 64 + 8 * c);
       const uint4 ra = rp[odd ? 1 : 0], rb = rp[odd ? 0 : 1];
       const uint4 lo = odd ? rb : ra, hi = odd ? ra : rb;
@@ -1059,13 +854,11 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       // LUT index of every period byte v: v ^ 3 (v >> 5), a bijection that
       // puts the common bytes (all composite, one prime) in distinct banks
       // (indexed by v, 255 / 223 / 191 / 127 would share bank 31)
-#if DSE_LUT_GLOBAL != 2  // (2: the global table is indexed by v itself: no banks to spread)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const uint32_t h = (W[j] >> 5) & 0x07070707u;
         W[j] ^= h + (h << 1);  // 3h <= 21: no carry into the next byte
       }
-#endif
       uint32_t o[15];
 #pragma unroll
       for (int w = 0; w < 15; ++w) o[w] = 0;
@@ -1073,11 +866,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       for (int q = 0; q < 4; ++q) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-#if DSE_LUT_GLOBAL
-          const uint32_t e = g_lut[(W[j] >> (8 * q)) & 0xFFu];  // vector L1: no LDS bank conflicts
-#else
           const uint32_t e = s_lut[(W[j] >> (8 * q)) & 0xFFu];
-#endif
           const int pos = 15 * (8 * q + j);
           o[pos >> 5] |= e << (pos & 31);
           if ((pos & 31) > 17) o[(pos >> 5) + 1] |= e >> (32 - (pos & 31));
@@ -1091,7 +880,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
 #pragma unroll
         for (int w = 0; w < 15; ++w) cnt += __popc(o[w]);
         my_count += cnt;
-        if (out && (phases & kPhaseStore)) {
+        if (out) {
 #pragma unroll
           for (int w = 0; w < 15; ++w) out[w0 + w] = o[w];
         }
@@ -1105,7 +894,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
           cnt += __popc(o[w]);
         }
         my_count += cnt;
-        if (out && (phases & kPhaseStore)) {
+        if (out) {
 #pragma unroll
           for (int w = 0; w < 15; ++w)
             if (w0 + w < out_words) out[w0 + w] = o[w];
@@ -1114,8 +903,8 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     }
   };
 
-  // ---- mark segment s into image img, units from counter ctr_i ------------
-  auto mark_segment = [&](uint32_t* __restrict__ img, uint64_t s, uint32_t ctr_i) {
+  // ---- mark segment s into image img -------------------------------------
+  auto mark_segment = [&](uint32_t* __restrict__ img, uint64_t s) {
     const uint64_t Vs = wa.V0 + s * kWheelSpan;  // segment base value
     const uint64_t Vend = Vs + kWheelSpan;
     // Lane-derived values are segment-invariant; left visible, the compiler
@@ -1131,7 +920,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     // units of kBkUnit entries, then one unit over the spill list if it is
     // not empty.
     uint32_t bk_b0 = 0, bk_b1 = 0, n0u = 0, n1u = 0, n3 = 0;
-    if (BK && (phases & kPhaseLarge)) {
+    if (BK) {
       n0u = wa.bk_k0 ? kBkGrid0 / kBk0Lists : 0u;
       bk_b0 = wa.bk_start[s];
       bk_b1 = wa.bk_start[s + 1];
@@ -1160,7 +949,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     // atomic optimizer aggregates it over the wave and waits for its return
     // on the spot (draining the previous unit's marks with it), which
     // defeats the two-ahead issue. Read through claimed().
-    const uint32_t ctr_addr = lds_addr(&lds.ctr[ctr_i]);
+    const uint32_t ctr_addr = lds_addr(&lds.ctr);
     auto claim = [&]() -> uint32_t {
       uint32_t j = 0;
       if (lane == 0) asm volatile("ds_add_rtn_u32 %0, %1, %2" : "=v"(j) : "v"(ctr_addr), "v"(1u) : "memory");
@@ -1181,16 +970,12 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     };
     auto bk_of = [&](uint32_t q) -> uint32_t { return q < 2 * mb ? q >> 1 : q - mb; };
     LargeOps cur, nxt;
-#if DSE_L_SETS == 2
     LargeOps cur1, nxt1;  // the unit's second 64 primes
-#endif
     uint32_t q_cur = claimed(claim());
     uint32_t q_nxt = claimed(claim());
     if (q_cur < n_q && unit_of(q_cur) != ~0u && is_l(unit_of(q_cur))) {
       load_L(cur, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_cur)) + lane, i_big);
-#if DSE_L_SETS == 2
       load_L(cur1, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_cur)) + 64 + lane, i_big);
-#endif
     }
     while (q_cur < n_q) {
       // issued and read in the same iteration: the asm output is written when
@@ -1200,9 +985,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       const uint32_t c2 = claim();  // unit after next, read at the end of this one
       if (q_nxt < n_q && unit_of(q_nxt) != ~0u && is_l(unit_of(q_nxt))) {
         load_L(nxt, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_nxt)) + lane, i_big);
-#if DSE_L_SETS == 2
         load_L(nxt1, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_nxt)) + 64 + lane, i_big);
-#endif
       }
       const uint32_t u_cur = unit_of(q_cur);
       if (BK && u_cur == ~0u) {  // a bucket unit, kBkBatchU loads in flight per lane
@@ -1216,7 +999,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
             const uint32_t* __restrict__ r[4];
 #pragma unroll
             for (uint32_t l = 0; l < 4; ++l) {
-              n[l] = (uint32_t)__builtin_amdgcn_readlane((int)nl, (int)(g + l));
+              n[l] = min((uint32_t)__builtin_amdgcn_readlane((int)nl, (int)(g + l)), wa.bk_k0);
               r[l] = wa.bk_reg0 + (li0 + g + l) * wa.bk_k0;
               nmax = max(nmax, n[l]);
             }
@@ -1253,116 +1036,53 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
           }
         }
         cur = nxt;
-#if DSE_L_SETS == 2
         cur1 = nxt1;
-#endif
         q_cur = q_nxt;
         q_nxt = claimed(c2);
         continue;
       }
       const uint32_t k = idx_of(u_cur);
-#ifdef DSE_TIMING
-      const uint64_t t_u0 = __builtin_amdgcn_s_memtime();
-      const uint32_t u_type = !is_l(u_cur) ? (k < nA ? 5u : 6u) : 7u;
-#endif
       if (!is_l(u_cur)) {
         if (k < nA) {
           const uint32_t pi = __builtin_amdgcn_readfirstlane(s_mid_p[k]);
           const uint32_t p = pi & 0xFFFFu;
           const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mid_m[k] >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_mid_m[k]);
-          if ((phases & kPhaseMidA) && (uint64_t)p * p < Vend) unit_A(img, pi, m, Vs, wa.rho_pack, lane, one);
+          if ((uint64_t)p * p < Vend) unit_A(img, pi, m, Vs, wa.rho_pack, lane, one);
         } else {
           const uint32_t j0 = nA + (k - nA) * 8;
           const uint32_t pf = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
-          if ((phases & kPhaseMidB) && (uint64_t)pf * pf < Vend)
+          if ((uint64_t)pf * pf < Vend)
             unit_B(img, s_mid_p, s_mid_m, j0, min(8u, n_mid - j0), Vs, Vend, wa.rho_pack, lane, one);
         }
       } else {
         const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p);
-        if ((phases & kPhaseLarge) && (uint64_t)p0 * p0 < Vend) unit_L(cur, Vs, Vend, Kb, ps, pl_rot, wa.rho_pack);
-#if DSE_L_SETS == 2
+        if ((uint64_t)p0 * p0 < Vend) unit_L(cur, Vs, Vend, Kb, ps, pl_rot, wa.rho_pack);
         const uint32_t p1 = __builtin_amdgcn_readfirstlane(cur1.p);
-        if ((phases & kPhaseLarge) && (uint64_t)p1 * p1 < Vend) unit_L(cur1, Vs, Vend, Kb, ps, pl_rot, wa.rho_pack);
-#endif
+        if ((uint64_t)p1 * p1 < Vend) unit_L(cur1, Vs, Vend, Kb, ps, pl_rot, wa.rho_pack);
       }
-#ifdef DSE_TIMING
-      lds_drain();
-      t_acc[u_type] += __builtin_amdgcn_s_memtime() - t_u0;
-#endif
       cur = nxt;
-#if DSE_L_SETS == 2
       cur1 = nxt1;
-#endif
       q_cur = q_nxt;
       q_nxt = claimed(c2);
     }
   };
 
-#if DSE_PIPELINE
-  if (T > 0) {
-    if (expander) init_segment(lds.img[0], blockIdx.x);
-    __syncthreads();
-    // round t: image t&1 is marked (segment of round t), image (t+1)&1 holds
-    // the segment of round t-1 (expanded, then re-initialised for round t+1)
-    for (uint32_t t = 0; t <= T; ++t) {
-      const uint32_t X = t & 1;
-      const uint64_t s = blockIdx.x + (uint64_t)t * grid;
-      if (expander) {
-        if (t >= 1 && (phases & kPhaseExpand)) expand_segment(lds.img[X ^ 1], s - grid);
-        if (t + 1 < T) init_segment(lds.img[X ^ 1], s + grid);
-        if (tid == 0) lds.ctr[X ^ 1] = 0;  // round t+1's counter; its last claims were in round t-1
-      }
-      if (t < T && (phases & kPhaseUnits)) mark_segment(lds.img[X], s, X);
-      lds_drain();
-      __syncthreads();
-    }
-  }
-#else
-#if DSE_PRIO
-  const uint32_t wave_u = __builtin_amdgcn_readfirstlane(wave);
-  auto set_prio = [](uint32_t pr) {  // s_setprio takes an immediate
-    if (pr == 0) __builtin_amdgcn_s_setprio(0);
-    else if (pr == 1) __builtin_amdgcn_s_setprio(1);
-    else if (pr == 2) __builtin_amdgcn_s_setprio(2);
-    else __builtin_amdgcn_s_setprio(3);
-  };
-#if DSE_PRIO == 2
-  set_prio(wave_u >> 2);
-#endif
-#endif
-  if (T > 0) init_segment(lds.img[0], blockIdx.x);
+  if (T > 0) init_segment(lds.img, blockIdx.x);
   __syncthreads();
-  DSE_TSTAMP(0);
   for (uint32_t t = 0; t < T; ++t) {
     const uint64_t s = blockIdx.x + (uint64_t)t * grid;
-    if (phases & kPhaseUnits) mark_segment(lds.img[0], s, 0);
+    mark_segment(lds.img, s);
     lds_drain();
-    DSE_TSTAMP(1);
     __syncthreads();
-    DSE_TSTAMP(2);
-#if DSE_PRIO == 1
-    set_prio(wave_u >> 2);  // the statically split phase: younger waves (a SIMD's later ones) first
-#endif
-    if (phases & kPhaseExpand) expand_segment(lds.img[0], s);
-    DSE_TSTAMP(3);
+    expand_segment(lds.img, s);
     // init of this workgroup's next segment, on the rows this wave just
     // expanded: no barrier in between, and waves drift into init while
     // others still expand
-    if (t + 1 < T) init_segment(lds.img[0], s + grid);
-#if DSE_PRIO == 1
-    __builtin_amdgcn_s_setprio(0);
-#endif
-    if (tid == 0) lds.ctr[0] = 0;  // all claims of this segment returned before the barrier above
-    DSE_TSTAMP(4);
+    if (t + 1 < T) init_segment(lds.img, s + grid);
+    if (tid == 0) lds.ctr = 0;  // all claims of this segment returned before the barrier above
     __syncthreads();
-    DSE_TSTAMP(5);
   }
-#endif
-#ifdef DSE_TIMING
-  if (lane_id == 0)
-    for (int i = 0; i < 8; ++i) atomicAdd(&g_timing[i], (unsigned long long)t_acc[i]);
-#endif
 
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) my_count += __shfl_xor(my_count, o);
@@ -1401,15 +1121,9 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
   uint32_t* A = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + table_a_offset(h->cap));
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t p = P[i];
-#if DSE_BK_NO_M
     if (p > kWheelMaxPrime) continue;  // bucketed primes: the walks divide in double precision
     const uint64_t m = barrett_factor(p);
     M[i] = m;
-#else
-    const uint64_t m = barrett_factor(p);
-    M[i] = m;
-    if (p > kWheelMaxPrime) continue;  // bucketed primes: the walk needs m only, never the rows
-#endif
     if (p < 7) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) A[8ull * i + j] = 0;
@@ -1522,23 +1236,16 @@ __global__ __launch_bounds__(64) void bucket_range_kernel(const void* __restrict
 
 // First coprime-to-30 multiple of p at or above max(V0 + 1, p^2): its offset
 // o from V0 and 3 * (index of the multiplier mod 30 in R30).
-__device__ __forceinline__ uint64_t bucket_first(uint32_t p, uint64_t m, const BucketArgs& ba, uint32_t& w3) {
+__device__ __forceinline__ uint64_t bucket_first(uint32_t p, const BucketArgs& ba, uint32_t& w3) {
   const uint64_t p2 = (uint64_t)p * p;
   const uint64_t vlo = max(ba.V0 + 1, p2);
-#if DSE_BK_NO_M
   // floor(vlo / p) from a double quotient: vlo < 2^62 rounds by < 2^9 and
   // p > 2^20, so the estimate is within 1 of the truth; corrected exactly
-  (void)m;
   uint64_t q = (uint64_t)((double)vlo / (double)p);
   int64_t rs = (int64_t)(vlo - q * p);
   while (rs < 0) { rs += p; --q; }
   while (rs >= (int64_t)p) { rs -= p; ++q; }
-  uint64_t r = (uint64_t)rs;
-#else
-  uint64_t q = __umul64hi(vlo, m);  // floor(vlo / p), corrected
-  uint64_t r = vlo - q * p;
-  while (r >= p) { r -= p; ++q; }
-#endif
+  const uint64_t r = (uint64_t)rs;
   const uint64_t m0 = q + (r != 0);
   const uint32_t r30 = (uint32_t)(m0 % 30);
   const uint32_t d = __builtin_ctz(kCoprime30 >> r30);
@@ -1561,48 +1268,32 @@ __device__ __forceinline__ uint32_t bucket_entry(uint64_t o, const BucketArgs& b
   return (word << 5) | (k & 31u);
 }
 
-#ifndef DSE_BK_SNAKE
-#define DSE_BK_SNAKE 1  // 0: band 0 in plain grid-stride order (A/B)
-#endif
 // Grid-strided walk (workgroup b of its band) over this thread's bucketed
-// primes [i_lo, i_hi): each prime's (p, m) is loaded one prime ahead, so the
-// load's latency hides behind the previous prime's walk (loaded on demand, a
+// primes [i_lo, i_hi): each prime is loaded one prime ahead, so the load's
+// latency hides behind the previous prime's walk (loaded on demand, a
 // thread's ~200 primes were a chain of dependent global loads: ~0.7 ms per
-// walk at the 1e18 window). snake: odd rounds of the stride take their block
-// in reverse thread order, so the thread with one round's smallest prime (the
-// most hits, ~1/p) gets the next round's largest; in plain order the threads
-// holding a band's smallest primes walk up to ~1.7x the mean.
+// walk at the 1e18 window).
 template <typename Walk>
-__device__ __forceinline__ void for_bucket_primes(const uint32_t* __restrict__ P, const uint64_t* __restrict__ M,
-                                                  uint32_t i_lo, uint32_t i_hi, uint32_t b, uint32_t stride,
-                                                  bool snake, Walk walk) {
-  const uint32_t j = b * kBucketThreads + threadIdx.x;
-  const uint32_t jr = DSE_BK_SNAKE && snake ? stride - 1 - j : j;
-  uint32_t base = i_lo, i = i_lo + j;
+__device__ __forceinline__ void for_bucket_primes(const uint32_t* __restrict__ P, uint32_t i_lo, uint32_t i_hi,
+                                                  uint32_t b, uint32_t stride, Walk walk) {
+  uint32_t i = i_lo + b * kBucketThreads + threadIdx.x;
   if (i >= i_hi) return;
   uint32_t pn = P[i];
-  uint64_t mn = DSE_BK_NO_M ? 0 : M[i];
-  for (bool odd = false;;) {  // round indices increase, so the first one past i_hi ends the walk
+  for (;;) {
     const uint32_t p = pn;
-    const uint64_t m = mn;
-    base += stride;
-    odd = !odd;
-    i = base + (odd ? jr : j);
+    i += stride;
     const bool more = i < i_hi;
-    if (more) {
-      pn = P[i];
-      mn = DSE_BK_NO_M ? 0 : M[i];
-    }
-    walk(p, m);
+    if (more) pn = P[i];
+    walk(p);
     if (!more) break;
   }
 }
 
 // Walk the coprime-to-30 multiples of p inside [V0 + 1, V0 + span), from p^2 on.
 template <typename Emit>
-__device__ __forceinline__ void bucket_walk(uint32_t p, uint64_t m, const BucketArgs& ba, Emit emit) {
+__device__ __forceinline__ void bucket_walk(uint32_t p, const BucketArgs& ba, Emit emit) {
   uint32_t w3;
-  uint64_t o = bucket_first(p, m, ba, w3);
+  uint64_t o = bucket_first(p, ba, w3);
   while (o < ba.span) {
     uint32_t s;
     const uint32_t e = bucket_entry(o, ba, s);
@@ -1616,15 +1307,12 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_count_kernel(const void
                                                                     const uint32_t* __restrict__ range,
                                                                     uint32_t* __restrict__ cols) {
   extern __shared__ uint32_t cnt[];  // [nseg]
-  const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
   const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
-  const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
   for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) cnt[j] = 0;
   __syncthreads();
   // band-1 workgroup x: column x
-  for_bucket_primes(P, M, range[2], range[1], blockIdx.x, kBucketGrid1 * kBucketThreads, false,
-                    [&](uint32_t p, uint64_t m) {
-    bucket_walk(p, m, ba, [&](uint32_t sg, uint32_t) { atomicAdd(&cnt[sg], 1u); });
+  for_bucket_primes(P, range[2], range[1], blockIdx.x, kBucketGrid1 * kBucketThreads, [&](uint32_t p) {
+    bucket_walk(p, ba, [&](uint32_t sg, uint32_t) { atomicAdd(&cnt[sg], 1u); });
   });
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) cols[(uint64_t)j * kBucketCols + blockIdx.x] = cnt[j];
@@ -1658,8 +1346,9 @@ __global__ __launch_bounds__(256) void bucket_colscan_kernel(uint32_t* __restric
 
 // exclusive scan of the segment totals -> start[0..nseg]. A total above the
 // entry capacity (a rigorous bound, so never expected) sets *flag: the fill,
-// stage and sort kernels of the pass then skip, every segment's list is left
-// empty (start[] all 0) and the pass's count gets bit 63 set, so neither an
+// stage and sort kernels of the pass then skip (the fill only zeroing its
+// band-0 region fills), every segment's list is left empty (start[] all 0,
+// n0[] all 0) and the pass's count gets bit 63 set, so neither an
 // out-of-bounds store nor a silently wrong count can result; the host entry
 // points report it as DSE_EINTERNAL (dse_device_status).
 __global__ __launch_bounds__(1024) void bucket_startscan_kernel(const uint32_t* __restrict__ tot, uint32_t nseg,
@@ -1700,12 +1389,12 @@ __global__ __launch_bounds__(1024) void bucket_startscan_kernel(const uint32_t* 
 }
 
 #ifndef DSE_BK_CHUNK
-#define DSE_BK_CHUNK 32  // band-0 fill walks chunks of this many segments (0: prime by prime, A/B)
+#define DSE_BK_CHUNK 32  // band-0 fill walks chunks of this many segments
 #endif
 #ifndef DSE_BK_FILL_RG
 #define DSE_BK_FILL_RG 16
 #endif
-constexpr uint32_t kFillRG = DSE_BK_FILL_RG;  // stride rounds of primes walked together (DSE_BK_CHUNK)
+constexpr uint32_t kFillRG = DSE_BK_FILL_RG;  // stride rounds of primes walked together
 
 // Band 0, one-level fill: every hit is one dword store at its slot. Workgroup
 // b owns region (s, b) of every segment s: k0 slots at reg0 + (s kBucketGrid +
@@ -1722,9 +1411,7 @@ constexpr uint32_t kFillRG = DSE_BK_FILL_RG;  // stride rounds of primes walked 
 __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const void* __restrict__ table,
                                                const BucketArgs& ba, const uint32_t* __restrict__ range,
                                                const BandZero& bz) {
-  const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
   const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
-  const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
   const uint32_t i_lo = range[0], i_hi = range[2];
   for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) cur[j] = 0;
   __syncthreads();
@@ -1742,14 +1429,17 @@ __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const 
       }
     }
   };
-#if DSE_BK_CHUNK
   // Segment-ordered walk: a thread walks its primes of kFillRG stride rounds
   // together, chunk by chunk of DSE_BK_CHUNK segments, so region (s, b) gets
   // its hits within one chunk's time (while its lines are still in the L2)
-  // instead of over the whole walk.
+  // instead of over the whole walk. Snake order: odd rounds of the stride
+  // take their block in reverse thread order, so the thread with one round's
+  // smallest prime (the most hits, ~1/p) gets the next round's largest (in
+  // plain order the threads holding a band's smallest primes walk up to
+  // ~1.7x the mean).
   constexpr uint32_t stride = kBucketGrid * kBucketThreads;
   const uint32_t j = b * kBucketThreads + threadIdx.x;
-  const uint32_t jr = DSE_BK_SNAKE ? stride - 1 - j : j;
+  const uint32_t jr = stride - 1 - j;
   const uint64_t chunk = (uint64_t)DSE_BK_CHUNK * kWheelSpan;
   for (uint64_t r0 = 0; i_lo + r0 * stride < i_hi; r0 += kFillRG) {
     uint64_t o[kFillRG];
@@ -1762,7 +1452,7 @@ __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const 
       w3[r] = 0;
       if (i < i_hi) {
         pr[r] = P[i];
-        o[r] = bucket_first(pr[r], DSE_BK_NO_M ? 0 : M[i], ba, w3[r]);
+        o[r] = bucket_first(pr[r], ba, w3[r]);
       }
     }
     for (uint64_t end = chunk;; end += chunk) {
@@ -1782,11 +1472,6 @@ __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const 
       if (!left) break;
     }
   }
-#else
-  if (i_lo < i_hi)
-    for_bucket_primes(P, M, i_lo, i_hi, b, kBucketGrid * kBucketThreads, true,
-                      [&](uint32_t p, uint64_t m) { bucket_walk(p, m, ba, emit); });
-#endif
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) bz.n0[(uint64_t)j * kBucketGrid + b] = min(cur[j], bz.k0);
 }
@@ -1857,28 +1542,17 @@ __device__ __forceinline__ void bucket_stage_wg(uint32_t* sm, uint32_t b, const 
     atomicAdd(&cur[s >> kSupLog], cols[(uint64_t)s * kBucketCols + b]);
   __syncthreads();
 
-  const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
   const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
-  const uint64_t* M = reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
-  uint32_t pn = 0;
-  uint64_t mn = 0;
-  if (i < i_hi) {
-    pn = P[i];
-    mn = DSE_BK_NO_M ? 0 : M[i];
-  }
+  uint32_t pn = i < i_hi ? P[i] : 0u;
   uint32_t p = 0, w3 = 0;
   uint64_t o = ba.span;
   // next prime of this lane with a hit in the pass (o >= span: none left)
   auto next_prime = [&]() {
     while (i < i_hi) {
       p = pn;
-      const uint64_t m = mn;
       i += stride;
-      if (i < i_hi) {
-        pn = P[i];
-        mn = DSE_BK_NO_M ? 0 : M[i];
-      }
-      o = bucket_first(p, m, ba, w3);
+      if (i < i_hi) pn = P[i];
+      o = bucket_first(p, ba, w3);
       if (o < ba.span) return;
     }
     o = ba.span;
@@ -1934,34 +1608,16 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_fill_stage_kernel(
     const uint32_t* __restrict__ cols, const uint32_t* __restrict__ start, BandZero bz,
     uint32_t* __restrict__ tmp, uint32_t nsup, uint32_t nfill, const uint32_t* __restrict__ flag) {
   extern __shared__ uint32_t sm[];
-  if (flag[1]) return;  // capacity overflow (bucket_startscan_kernel)
   const uint32_t x = blockIdx.x;
+  if (flag[1]) {  // capacity overflow (bucket_startscan_kernel): no hits, but every band-0 region empty
+    if (x < nfill)
+      for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) bz.n0[(uint64_t)j * kBucketGrid + x] = 0;
+    return;
+  }
   if (x < nfill)
     bucket_fill_wg(sm, x, table, ba, range, bz);
   else
     bucket_stage_wg(sm, x - nfill, table, ba, range, cols, start, tmp, nsup);
-}
-
-#ifndef DSE_BK_SPLIT_KERNELS
-#define DSE_BK_SPLIT_KERNELS 0  // 1: band-0 fill and band-1 stage as two kernels (own register allocations) (A/B)
-#endif
-// The two halves of bucket_fill_stage_kernel as kernels of their own: the
-// band-0 walk's round state (16 rounds in registers) does not then set the
-// stage's register allocation and occupancy.
-__global__ __launch_bounds__(kBucketThreads) void bucket_fill0_kernel(const void* __restrict__ table, BucketArgs ba,
-                                                                    const uint32_t* __restrict__ range, BandZero bz,
-                                                                    const uint32_t* __restrict__ flag) {
-  extern __shared__ uint32_t sm[];
-  if (flag[1]) return;
-  bucket_fill_wg(sm, blockIdx.x, table, ba, range, bz);
-}
-__global__ __launch_bounds__(kBucketThreads) void bucket_stage1_kernel(
-    const void* __restrict__ table, BucketArgs ba, const uint32_t* __restrict__ range,
-    const uint32_t* __restrict__ cols, const uint32_t* __restrict__ start, uint32_t* __restrict__ tmp,
-    uint32_t nsup, const uint32_t* __restrict__ flag) {
-  extern __shared__ uint32_t sm[];
-  if (flag[1]) return;
-  bucket_stage_wg(sm, blockIdx.x, table, ba, range, cols, start, tmp, nsup);
 }
 
 __global__ __launch_bounds__(kSortThreads) void bucket_sort_kernel(BucketArgs ba, const uint32_t* __restrict__ cols,
@@ -2058,25 +1714,6 @@ __global__ __launch_bounds__(kSortThreads) void bucket_sort_kernel(BucketArgs ba
 #endif  // DSE_WHEEL_MAIN_TU
 }  // namespace
 
-#ifdef DSE_TIMING
-// profiling builds only: each wheel TU (main, plain, half) has its own g_timing;
-// read it, add it into acc and clear it
-#if DSE_WHEEL_PLAIN_TU
-int timing_take_plain(unsigned long long* acc) {
-#elif DSE_WHEEL_HALF_TU
-int timing_take_half(unsigned long long* acc) {
-#else
-int timing_take_plain(unsigned long long* acc);
-int timing_take_half(unsigned long long* acc);
-int timing_take_main(unsigned long long* acc) {
-#endif
-  unsigned long long t[8];
-  if (hipMemcpyFromSymbol(t, HIP_SYMBOL(g_timing), sizeof(t)) != hipSuccess) return -1;
-  for (int i = 0; i < 8; ++i) acc[i] += t[i];
-  const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_timing), z, sizeof(z)) == hipSuccess ? 0 : -1;
-}
-#endif
 
 #if DSE_WHEEL_MAIN_TU
 hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream, uint64_t n_hint) {
@@ -2085,13 +1722,6 @@ hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream, ui
   return hipGetLastError();
 }
 
-#ifdef DSE_TIMING
-// profiling builds only: read and clear the per-phase cycle sums of all three wheel TUs
-extern "C" int dse_debug_timing(unsigned long long* out) {
-  for (int i = 0; i < 8; ++i) out[i] = 0;
-  return (timing_take_main(out) || timing_take_plain(out) || timing_take_half(out)) ? -1 : 0;
-}
-#endif
 
 hipError_t free_scratch(Scratch* s) {
   if (!s) return hipSuccess;
@@ -2110,21 +1740,9 @@ hipError_t free_scratch(Scratch* s) {
 
 namespace {
 
-#ifdef DSE_PHASE_KNOB
-// Ablation builds only (tools/build_variant.sh knob -DDSE_PHASE_KNOB): the
-// DSE_PHASES bitmask switches kernel phases off. The production library reads
-// no environment variable.
-uint32_t knob_phases() {
-  static const uint32_t v = [] {
-    const char* e = getenv("DSE_PHASES");
-    return e ? (uint32_t)strtoul(e, nullptr, 0) & kPhaseAll : kPhaseAll;
-  }();
-  return v;
-}
-#endif
 
 // Launch geometry shared by the wheel kernel and the bucket walks.
-WheelArgs make_wheel_args(uint64_t g_start, uint64_t nbits, uint64_t* plane_lut) {
+[[maybe_unused]] WheelArgs make_wheel_args(uint64_t g_start, uint64_t nbits, uint64_t* plane_lut) {
   WheelArgs wa{};
   const uint64_t v_start = 3 + 2 * g_start;
   wa.V0 = v_start - 1;
@@ -2162,17 +1780,11 @@ WheelArgs make_wheel_args(uint64_t g_start, uint64_t nbits, uint64_t* plane_lut)
     return c;
   }();
   for (int t = 0; t < 4; ++t) wa.nthr[t] = counts[t];
-  for (int j = 0; j < kNQ; ++j) wa.v0q[j] = (uint8_t)(wa.V0 % kQ[j]);
   for (int g = 0; g < kNG; ++g) wa.v0g[g] = (uint16_t)(wa.V0 % gmod(g));
-#ifdef DSE_PHASE_KNOB
-  wa.phases = knob_phases();
-#else
-  wa.phases = kPhaseAll;
-#endif
   return wa;
 }
 
-uint64_t isqrt64(uint64_t x) {
+[[maybe_unused]] uint64_t isqrt64(uint64_t x) {
   uint64_t r = (uint64_t)__builtin_sqrt((double)x);
   while (r * r > x) --r;
   while ((r + 1) * (r + 1) <= x) ++r;
@@ -2367,6 +1979,14 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     char* sc = nullptr;
     hipError_t e = ensure_scratch(scratch, bytes, stream, &sc);
     if (e != hipSuccess) return e;
+    // from here on kernels may read the scratch: every exit records `done`
+    // (a later grow frees the buffer only after it)
+    auto fail_pass = [&](hipError_t err) {
+      (void)release_scratch(scratch, stream);
+      return err;
+    };
+    if (opts && opts->scratch_poison && (e = hipMemsetAsync(sc, 0xFF, bytes, stream)) != hipSuccess)
+      return fail_pass(e);  // test-only: stale scratch contents
     uint32_t* range = reinterpret_cast<uint32_t*>(sc);
     uint32_t* cols = reinterpret_cast<uint32_t*>(sc + o_cols);
     uint32_t* tot = reinterpret_cast<uint32_t*>(sc + o_tot);
@@ -2395,34 +2015,14 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     if (lds_bytes > 65536 &&
         (e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bucket_fill_stage_kernel),
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes)) != hipSuccess)
-      return e;
-#if DSE_BK_SPLIT_KERNELS
-    {
-      const uint32_t l0 = 4 * (uint32_t)ns, l1 = 4 * stage_lds_words(nsup);
-      if (band1 && l1 > 65536 &&
-          (e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bucket_stage1_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)l1)) != hipSuccess)
-        return e;
-      if (band0 && l0 > 65536 &&
-          (e = hipFuncSetAttribute(reinterpret_cast<const void*>(&bucket_fill0_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)l0)) != hipSuccess)
-        return e;
-      if (band1)
-        hipLaunchKernelGGL(bucket_stage1_kernel, dim3(kBucketGrid1), dim3(kBucketThreads), l1, stream, table, ba,
-                           range, cols, start, tmp, nsup, scratch->flag);
-      if (band0)
-        hipLaunchKernelGGL(bucket_fill0_kernel, dim3(kBucketGrid), dim3(kBucketThreads), l0, stream, table, ba, range,
-                           bz, scratch->flag);
-    }
-#else
+      return fail_pass(e);
     hipLaunchKernelGGL(bucket_fill_stage_kernel, dim3(nfill + (band1 ? kBucketGrid1 : 0)), dim3(kBucketThreads),
                        lds_bytes, stream, table, ba, range, cols, start, bz, tmp, nsup, nfill, scratch->flag);
-#endif
     if (band1) {
       hipLaunchKernelGGL(bucket_sort_kernel, dim3(nsup * (kBucketGrid1 / kSortGroup)), dim3(kSortThreads), 0,
                          stream, ba, cols, start, tmp, ent, scratch->flag);
     }
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipGetLastError()) != hipSuccess) return fail_pass(e);
     wa.bk_entries = ent;
     wa.bk_start = start;
     wa.bk_reg0 = bz.reg0;
@@ -2433,7 +2033,7 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     wa.bk_k0 = k0;
     if ((e = launch_wheel(table, wa, out ? out + s0 * (kWheelOutBits / 32) : nullptr, count, num_cus, stream)) !=
         hipSuccess)
-      return e;
+      return fail_pass(e);
     if ((e = release_scratch(scratch, stream)) != hipSuccess) return e;
     s0 += ns;
   }

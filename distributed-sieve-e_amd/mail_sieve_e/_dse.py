@@ -55,6 +55,7 @@ SIGNATURES = {
     "dse_sieve_range_dev_async": (_i32, [_vp, _vp, _u64, _u64, _vp, _vp, _vp]),
     "dse_device_status": (_i32, [_vp]),
     "dse_debug_set_option": (_i32, [_vp, _cp, _i64]),
+    "dse_debug_init_logical": (_vp, [_i32]),
 }
 
 _lib = None

@@ -28,11 +28,16 @@ from ._dse import check, lib, u64p
 
 class Context:
     """A libdse context: one process driving ``num_gpus`` devices, or one
-    device (``device=``) for one-process-per-GPU ranks."""
+    device (``device=``) for one-process-per-GPU ranks. ``logical=k`` (tests
+    only, include/dse.h dse_debug_init_logical): k logical devices on device 0,
+    the multi-device code path with the collectives replaced by copies."""
 
-    def __init__(self, num_gpus: int = 1, device: Optional[int] = None):
+    def __init__(self, num_gpus: int = 1, device: Optional[int] = None, logical: Optional[int] = None):
         L = lib()
-        self._ptr = L.dse_init_device(device) if device is not None else L.dse_init(num_gpus)
+        if logical is not None:
+            self._ptr = L.dse_debug_init_logical(logical)
+        else:
+            self._ptr = L.dse_init_device(device) if device is not None else L.dse_init(num_gpus)
         if not self._ptr:
             raise _dse.DseError(L.dse_last_status(), "dse_init", L.dse_last_error().decode(errors="replace"))
 

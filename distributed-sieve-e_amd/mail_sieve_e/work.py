@@ -24,6 +24,11 @@ BYTES_PER_MARK = 8
 # wave-instruction, MI355X_MICROARCH.md section LDS), 39,322 GB/s chip-wide.
 LDS_OR_BYTES_PER_MARK = 4
 LDS_OR_PEAK_GBS = NUM_CUS * 64 * CLOCK_HZ / 1e9    # 39,322 GB/s
+# The measured conflict-free ds_or_b32 rate: 2.6 CU-cycles per wave-instruction
+# (profiles/r02/lds_conflict_microbench.txt), i.e. 256 B / 2.6 clk / CU,
+# 60,494 GB/s chip-wide -- the peak the mark instruction itself reaches.
+DS_OR_CYCLES_PER_WAVE_INSTR = 2.6
+LDS_DS_OR_PEAK_GBS = NUM_CUS * 256 / DS_OR_CYCLES_PER_WAVE_INSTR * CLOCK_HZ / 1e9
 # VALU ceiling: a wave64 VALU instruction issues over 2 cycles on each of the
 # 4 SIMD-32 of a CU (MI355X_MICROARCH.md "Wave scheduling"): 2.0 per CU-cycle.
 VALU_PEAK_PER_CU_CYCLE = 2.0

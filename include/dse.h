@@ -193,8 +193,22 @@ int32_t dse_device_status(dse_ctx *ctx);
  *   "bucket_k0_divisor" = d >= 0: divide the band-0 region capacity by d
  *   (> 1), so hits go through the spill list (results unchanged); 0 or 1 =
  *   default.
+ *   "scratch_poison" = 1: fill the bucket scratch with 0xFF bytes before
+ *   every bucketed pass (stale contents: results unchanged, and an overflowed
+ *   pass still reads only what it wrote); 0 = default.
  * DSE_EINVAL for an unknown name or a value out of range. */
 int32_t dse_debug_set_option(dse_ctx *ctx, const char *name, int64_t value);
+
+/* A context of num_logical devices that all run on device 0 (each its own
+ * stream, table, counts, masks, scratch and side streams), so the multi-device
+ * code of dse_sieve_all / dse_sieve_window -- chunk map, table completion on
+ * the non-root devices, tail on the last device, flag checks -- runs on a
+ * one-GPU box. Only the two RCCL collectives are replaced: the broadcast of
+ * the primes by a device-to-device copy from device 0's table, the count
+ * all-reduce by a gather + sum on device 0 and a copy back, each ordered
+ * with events exactly where the RCCL calls would run. Test-only; NULL on
+ * failure (dse_last_status). */
+dse_ctx *dse_debug_init_logical(int32_t num_logical);
 
 #ifdef __cplusplus
 }

@@ -29,6 +29,10 @@ def _check_line(d: dict, n_gpus: int):
         assert k in rf, k
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-6 * rf["frac"] + 1e-12
     assert 0 < rf["frac"] <= 1
+    assert 0 < rf["frac_ds_or"] < rf["frac"] and rf["cycles_per_mark_instr"] > 2.6
+    # the world the run formed: one entry per rank
+    w = d["world"]
+    assert w["size"] == n_gpus and [x["rank"] for x in w["ranks"]] == list(range(n_gpus))
     # the headline is the median of per-step times, each from the call to the counts on the host
     assert d["ms_per_step"] > 0 and d["ms_per_step_bracketed"] > 0 and d["ms_per_step_pipelined"] > 0
     assert abs(d["value"] - d["config"]["N"] / (d["ms_per_step"] / 1e3)) < 1e-6 * d["value"]

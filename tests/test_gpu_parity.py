@@ -427,7 +427,7 @@ def test_debug_option_rejects_unknown(ctx):
         ctx.debug_set_option("no_such_option", 1)
     for name, bad in (("bucket_split_log2", 64), ("bucket_split_log2", -1), ("bucket_pass_segments", -1),
                       ("bucket_cap_divisor", -1), ("bucket_k0_divisor", -1), ("wheel_geometry", 3),
-                      ("wheel_geometry", -1)):
+                      ("wheel_geometry", -1), ("scratch_poison", 2), ("scratch_poison", -1)):
         with pytest.raises(_dse.DseError):
             ctx.debug_set_option(name, bad)
 
@@ -466,6 +466,32 @@ def test_bucket_overflow_flag(oracle):
         c.debug_set_option("bucket_cap_divisor", 0)
         m, cnt2 = c.sieve_odd_range(g0, nb)
         assert cnt2 == c_ref and np.array_equal(m, m_ref)
+
+
+def test_bucket_overflow_stale_scratch(oracle):
+    """an overflowed pass right after a scratch grow, with the
+    scratch full of stale bytes (test-only option scratch_poison): the fill
+    kernel still zeroes every band-0 region fill and the wheel kernel clamps
+    them, so the pass reads only what it wrote -- DSE_EINTERNAL, no fault --
+    and the same context is bit-exact afterwards (poisoned scratch, no
+    overflow: every pass rewrites what it reads)."""
+    from mail_sieve_e import _dse
+    from mail_sieve_e import sieve as S
+    g0, nb = (10**15 + 1 - 3) // 2, 3 * 10**6
+    m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
+    with S.Context(num_gpus=1) as c:
+        c.debug_set_option("scratch_poison", 1)
+        c.debug_set_option("bucket_split_log2", 22)  # both bands in the pass
+        c.debug_set_option("bucket_cap_divisor", 1000)
+        with pytest.raises(_dse.DseError) as e:
+            c.sieve_odd_range(g0, nb)  # first pass of the context: a fresh (grown) scratch
+        assert e.value.code == -7
+        c.debug_set_option("bucket_cap_divisor", 0)
+        m, cnt = c.sieve_odd_range(g0, nb)
+        assert cnt == c_ref and np.array_equal(m, m_ref)
+        c.debug_set_option("bucket_split_log2", 0)
+        m, cnt = c.sieve_odd_range(g0, nb)
+        assert cnt == c_ref and np.array_equal(m, m_ref)
 
 
 @pytest.mark.parametrize("div", [8, 100000])
