@@ -77,15 +77,8 @@ struct DevState {
   uint64_t scratch_words = 0;
   std::vector<ChunkMask> resident;       // masks kept by dse_sieve_all
   dse::Scratch scratch;                  // bucketed-pass scratch (high-offset ranges)
-  // Several chunks on one device (dse_sieve_all with P > devices): each
-  // chunk's launch goes to its own stream, so the workgroups of the next
-  // chunk fill the CUs that the last, partial round of a chunk leaves idle.
-  std::vector<hipStream_t> side;         // up to kSideStreams, created on first use
-  std::vector<hipEvent_t> side_done;     // one per side stream
-  hipEvent_t ready = nullptr;            // the table (and zeroed counts) on `stream`
   hipEvent_t xev = nullptr;              // logical devices: this device's side of a collective
 };
-constexpr size_t kSideStreams = 4;       // the runtime's hardware queues per process (GPU_MAX_HW_QUEUES)
 
 }  // namespace
 
@@ -159,19 +152,6 @@ int32_t check_flag(DevState& d, uint32_t h) {
   HIP_TRY(hipStreamSynchronize(d.stream));
   return fail(DSE_EINTERNAL, "bucketed pass exceeded its entry capacity on device " + std::to_string(d.device) +
                                  "; the count and mask of this call are not valid");
-}
-
-int32_t ensure_side_streams(DevState& d) {
-  if (!d.ready) HIP_TRY(hipEventCreateWithFlags(&d.ready, hipEventDisableTiming));
-  while (d.side.size() < kSideStreams) {
-    hipStream_t st;
-    hipEvent_t ev;
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    d.side.push_back(st);
-    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    d.side_done.push_back(ev);
-  }
-  return DSE_OK;
 }
 
 int32_t free_resident(DevState& d) {
@@ -364,9 +344,6 @@ void dse_destroy(dse_ctx* ctx) {
     if (d.counts) (void)hipFree(d.counts);
     if (d.scratch_mask) (void)hipFree(d.scratch_mask);
     (void)dse::free_scratch(&d.scratch);
-    for (auto st : d.side) (void)hipStreamDestroy(st);
-    for (auto ev : d.side_done) (void)hipEventDestroy(ev);
-    if (d.ready) (void)hipEventDestroy(d.ready);
     if (d.xev) (void)hipEventDestroy(d.xev);
     if (d.stream) (void)hipStreamDestroy(d.stream);
   }
@@ -568,34 +545,19 @@ int32_t dse_sieve_all(dse_ctx* ctx, int64_t n, int32_t P, uint64_t* per_chunk_co
   if ((rc = share_table(ctx, limit))) return rc;
 
   // each device sieves its chunks; the last device also sieves the tail.
-  // With several chunks on a device they go to side streams (round robin),
-  // each waiting for the table, and the device's stream waits for them all
-  // (bucketed passes stay ordered through the scratch's event).
+  // All of a device's ranges go to one launch_sieve_ranges call: its chunks
+  // (and the tail) share persistent launches of the wheel kernel, so no
+  // chunk's partial last round leaves the CUs idle and no host launch sits
+  // between chunks.
   for (int i = 0; i < nd; ++i) {
     DevState& d = ctx->devs[i];
     HIP_TRY(hipSetDevice(d.device));
-    const size_t jobs = d.resident.size() + (i == nd - 1 && tail_n ? 1 : 0);
-    const bool multi = jobs > 1;
-    if (multi) {
-      if ((rc = ensure_side_streams(d))) return rc;
-      HIP_TRY(hipEventRecord(d.ready, d.stream));
-      for (auto st : d.side) HIP_TRY(hipStreamWaitEvent(st, d.ready, 0));
-    }
-    size_t j = 0;
-    auto stream_for = [&](size_t jj) { return multi ? d.side[jj % d.side.size()] : d.stream; };
-    for (auto& cm : d.resident) {
-      const uint64_t g0 = (uint64_t)(cm.my_num - 1) * (uint64_t)cs;
-      HIP_TRY(dse::launch_sieve_range(d.table, g0, (uint64_t)cs, reinterpret_cast<uint32_t*>(cm.dev_ptr),
-                                      d.counts + (cm.my_num - 1), d.num_cus, stream_for(j++), &d.scratch, &ctx->opts));
-    }
-    if (i == nd - 1 && tail_n)
-      HIP_TRY(dse::launch_sieve_range(d.table, tail_g, tail_n, nullptr, d.counts + P, d.num_cus, stream_for(j++),
-                                      &d.scratch, &ctx->opts));
-    if (multi)
-      for (size_t k = 0; k < d.side.size(); ++k) {
-        HIP_TRY(hipEventRecord(d.side_done[k], d.side[k]));
-        HIP_TRY(hipStreamWaitEvent(d.stream, d.side_done[k], 0));
-      }
+    std::vector<dse::RangeSpec> rs;
+    for (auto& cm : d.resident)
+      rs.push_back({(uint64_t)(cm.my_num - 1) * (uint64_t)cs, (uint64_t)cs, reinterpret_cast<uint32_t*>(cm.dev_ptr),
+                    d.counts + (cm.my_num - 1)});
+    if (i == nd - 1 && tail_n) rs.push_back({tail_g, tail_n, nullptr, d.counts + P});
+    HIP_TRY(dse::launch_sieve_ranges(d.table, rs.data(), rs.size(), d.num_cus, d.stream, &d.scratch, &ctx->opts));
   }
 
   // counts: RCCL all-reduce (each slot is non-zero on exactly one device)

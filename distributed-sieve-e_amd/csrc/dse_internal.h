@@ -88,6 +88,23 @@ hipError_t launch_sum_rows(const unsigned long long* in, uint32_t nsrc, uint32_t
 // above it a sieve of [3, limit] by the wheel kernel + ordered compaction.
 hipError_t launch_base_primes_big(uint64_t limit, void* table, uint32_t cap, int num_cus, hipStream_t stream);
 
+// One odd-index range [g_start, g_start + nbits) of a launch: out (may be
+// null) gets its mask as 32-bit words, *count (device) is incremented by its
+// primes.
+struct RangeSpec {
+  uint64_t g_start;
+  uint64_t nbits;
+  uint32_t* out;
+  unsigned long long* count;
+};
+
+// Sieve the ranges rs[0..n) on one stream: the ranges without bucketed primes
+// share persistent launches of the wheel kernel (several chunks of one
+// device: one launch, no idle partial rounds between them); ranges whose
+// sqrt(max value) exceeds kWheelMaxPrime run their bucketed passes one by one
+// (they need `scratch`). `opts` may be null. Empty ranges are skipped.
+hipError_t launch_sieve_ranges(const void* table, const RangeSpec* rs, size_t n, int num_cus, hipStream_t stream,
+                               Scratch* scratch, const SieveOpts* opts);
 // Sieve odd indices [g_start, g_start+nbits) with the mod-30 wheel kernel: out
 // (may be null) gets the mask as 32-bit words (2*ceil(nbits/64) of them, upper
 // half of the last uint64 zeroed); *count (device) is incremented. Ranges whose
@@ -97,14 +114,13 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
                               unsigned long long* count, int num_cus, hipStream_t stream, Scratch* scratch,
                               const SieveOpts* opts);
 // The same sieve with the half-size segment geometry (2^16 periods,
-// dse_wheel_half.hip): launch_sieve_range gives it the tail of a range whose
-// last round of full segments would leave most CUs idle. No bucketed primes.
-hipError_t launch_wheel_range_half(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
-                                   unsigned long long* count, int num_cus, hipStream_t stream);
+// dse_wheel_half.hip): launch_sieve_ranges gives it the segments past the last
+// full round of a launch when that finishes sooner. No bucketed primes.
+hipError_t launch_wheel_ranges_half(const void* table, const RangeSpec* rs, size_t n, int num_cus,
+                                    hipStream_t stream);
 // The full-geometry wheel kernel without bucketed primes (dse_wheel_plain.hip,
 // its own compile flags); wa points at the caller's WheelArgs (dse_wheel.hip).
-hipError_t launch_wheel_plain(const void* table, const void* wa, uint32_t* out, unsigned long long* count,
-                              int num_cus, hipStream_t stream);
+hipError_t launch_wheel_plain(const void* table, const void* wa, int num_cus, hipStream_t stream);
 // Fill the Barrett factors m[] and wheel offsets a[] of a table whose p[] is final.
 // n_hint: table capacity when known (sizes the grid: about 4 primes per thread)
 hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream, uint64_t n_hint = 0);

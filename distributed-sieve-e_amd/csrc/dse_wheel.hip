@@ -13,29 +13,36 @@
 // with gcd(V0 + rho, 30) = 1 define the planes: plane i bit k <-> the value
 // Vs + rho_i + 30k, i.e. output bit 15k + (rho_i - 1)/2 of the segment.
 //
-// LDS image (128 KiB): plane i is split into 8 columns of LS = KP/8 periods;
-// column C = 8c + i holds periods [c*LS, (c+1)*LS) of plane i, 32 per word,
-// and word (row r, column C) sits at r*64 + C: the 8 planes of one (row, c)
-// are 32 contiguous bytes (two ds_read_b128 in the expansion). The bank of a
-// word is C mod 32 whatever its row, so 32 lanes in 32 distinct columns mod 32
-// never conflict.
+// LDS image (128 KiB), word-interleaved: block R (periods 32R .. 32R+31)
+// is 8 consecutive words, one per plane, so the word of (plane i, period k)
+// is 8 (k >> 5) + i and its byte address (k & ~31) | 4i -- one v_and_or from
+// a period index, and an image of 2^17 periods is 2^17 bytes. The bank of a
+// ds_or_b32 (dword address mod 32) is 8 ((k >> 5) mod 4) + i, so a mark
+// pattern is conflict-free when the lanes on one plane in a 32-lane group sit
+// in distinct blocks mod 4; two lanes per bank cost nothing extra (the
+// instruction's transfer takes 2 LDS cycles per group anyway).
 //
 // One workgroup of 1024 threads per CU, segments blockIdx.x + t*gridDim.x.
 // Per segment:
 //   1. mark (ds_or_b32), units taken from one LDS counter:
-//      A (61 < p <= TA): one prime per wave, lane L walks column L;
-//      B (TA < p <= TB): 8 primes x 8 planes per wave; lane (prime j, plane i)
-//        walks its plane's 8 columns diagonally (column (j+t) mod 8 at step t);
-//        half-wave g holds primes 4g..4g+3, so its columns differ mod 32;
-//      L (p > TB): one prime per lane, its 8 planes in a lane-rotated order,
-//        starts from the table's wheel offsets with one reduction;
-//   2. expand: lane reads one row of its column in all 8 planes (two
-//      ds_read_b128), transposes the 8x32 bits into 32 period bytes, maps
-//      each through a 256-entry LDS table to the 15 odd slots of its period
-//      (composite bits in, prime slots out), packs 480 output bits, fixes
-//      the small primes 3..61, masks the range end, popcounts, stores; then
-//      each wave inits (patterns of 7..61) the rows it expanded, for the next
-//      segment.
+//      A  (61 < p <= TA): one prime per wave; lane (plane i, c = 0..7) takes
+//         the hits n of its plane with n mod 256 in [32c, 32c+32), by class
+//         n mod 256: a class's hits sit 256p periods apart, same bit, so each
+//         further mark is one v_add; the 4 lanes of a plane in a half-wave
+//         are 32p periods apart, i.e. in blocks c*p mod 4: distinct banks;
+//      B1 (TA < p <= TB1): one prime per half-wave; lane (plane i, j = 0..3)
+//         takes the hits n with n mod 128 in [32j, 32j+32), in order (3 VALU
+//         per mark), again 32p periods apart: conflict-free;
+//      B2 (TB1 < p <= TB): 8 primes x 8 planes per wave, lane (prime, plane)
+//         walks its plane's hits in order;
+//      L  (p > TB): one prime per lane, its 8 planes in a lane-rotated order,
+//         starts from the table's wheel offsets with one reduction;
+//   2. expand: lane reads one block (two ds_read_b128), transposes the 8x32
+//      bits into 32 period bytes, maps each through a 256-entry LDS table to
+//      the 15 odd slots of its period (composite bits in, prime slots out),
+//      packs 480 output bits, fixes the small primes 3..61, masks the range
+//      end, popcounts, stores; then each wave inits (patterns of 7..61) the
+//      blocks it expanded, for the next segment.
 // See DESIGN.md section 4 for the rooflines.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -52,13 +59,13 @@ namespace dse {
 namespace {
 
 constexpr uint32_t KP = 1u << kWheelLogKP;  // periods per segment (per plane)
-constexpr uint32_t LOG_LS = kWheelLogKP - 3;
-constexpr uint32_t LS = 1u << LOG_LS;       // periods per column
-constexpr uint32_t ROWS = LS / 32;          // words per column
-constexpr uint32_t IMG_WORDS = 64 * ROWS;   // one segment image
+constexpr uint32_t BLOCKS = KP / 32;        // 32-period blocks (8 words each)
+constexpr uint32_t IMG_WORDS = 8 * BLOCKS;  // one segment image
+constexpr uint32_t IMG_BYTES = 4 * IMG_WORDS;
+static_assert(IMG_BYTES == KP, "a period index is its block's byte address");
 constexpr uint32_t NT = 1024;
 constexpr uint32_t NW = NT / 64;            // waves; every wave marks, expands and inits
-static_assert(ROWS % (8 * NW) == 0, "expander rows");
+static_assert(BLOCKS % (64 * NW) == 0, "expansion blocks");
 #ifndef DSE_TA
 #define DSE_TA 256
 #endif
@@ -75,12 +82,16 @@ static_assert(ROWS % (8 * NW) == 0, "expander rows");
 #ifndef DSE_LAUNCH_COST
 #define DSE_LAUNCH_COST 0.1
 #endif
-constexpr uint32_t TA = DSE_TA;             // A/B threshold
+constexpr uint32_t TA = DSE_TA;             // A/B1 threshold
+#ifndef DSE_TB1
+#define DSE_TB1 1024
+#endif
+constexpr uint32_t TB1 = DSE_TB1;           // B1/B2 threshold
 #ifndef DSE_TB
 #define DSE_TB 4096
 #endif
-constexpr uint32_t TB = DSE_TB;             // B/L threshold (<= LS)
-static_assert(TB <= LS && TB >= TA, "B/L threshold");
+constexpr uint32_t TB = DSE_TB;             // B2/L threshold
+static_assert(TA <= 256 && TA < TB1 && TB1 <= TB && TB <= KP / 8, "unit thresholds");
 constexpr uint32_t kMidCap = TB >= 16384 ? 1920 : TB >= 8192 ? 1040 : TB >= 4096 ? 580 : 320;  // odd primes in (61, TB]
 constexpr uint32_t kOutWordsPerSeg = (uint32_t)(kWheelOutBits / 32);  // 30720
 
@@ -110,7 +121,9 @@ constexpr int kNG = 7;
 constexpr uint32_t kGQ[kNG][3] = {{7, 11, 13}, {17, 19, 1}, {23, 29, 1}, {31, 37, 1},
                                   {41, 43, 1}, {47, 53, 1}, {59, 61, 1}};
 constexpr uint32_t gmod(int g) { return kGQ[g][0] * kGQ[g][1] * kGQ[g][2]; }
-constexpr uint32_t kInitRun = 32 * (ROWS / NW);  // periods one lane inits per segment (one column)
+constexpr uint32_t kInitWords = IMG_WORDS / NT;  // words one lane inits per segment (one plane of a block run)
+constexpr uint32_t kInitRun = 32 * kInitWords;    // their periods
+constexpr uint32_t kExpandBlocks = BLOCKS / NW;   // blocks one wave expands (and inits) per segment
 constexpr uint32_t kInitBlocks = kInitRun / 128 + 1;  // ds_read_b128 per lane and group
 // dwords per group string and copy: the reads reach dword d0 + 4 kInitBlocks - 1, d0 < M_G/32 + 1
 constexpr uint32_t gdw(int g) { return ((gmod(g) + 32 * (4 * kInitBlocks + 1) + 127) / 128) * 4; }
@@ -143,16 +156,32 @@ constexpr InitTables make_init_tables() {
 }
 __device__ const InitTables g_init_tables = make_init_tables();
 
-struct WheelArgs {
+// One odd-index range of a launch: its segments are [seg0, seg0 + its
+// segment count) of the launch's list (WheelArgs::nseg in all).
+struct WheelRange {
   uint64_t V0;         // v_start - 1
   uint64_t nbits;      // odd candidates in the range
   uint64_t KB0;        // floor(V0 / 30)
   uint64_t rho_pack;   // rho_i in bits [5i, 5i+5)
+  uint32_t* out;       // the range's mask (32-bit words), or null
+  unsigned long long* count;  // incremented by the range's prime count (device)
   uint32_t pl_pack;    // plane of absolute residue R30[j] in bits [3j, 3j+3)
   uint32_t e_iota;     // bit j: floor((V0 + rho)/30) = KB0 + 1 for the plane of R30[j]
   uint32_t fix0;       // output word 0 bits of the primes 3..61 inside the range
+  uint32_t seg0;       // first segment of the range in the launch
   uint16_t v0g[kNG];   // V0 mod M_G (init tables)
-  uint32_t nthr[4];    // odd primes <= 61, <= TA, <= TB, <= kWheelMaxPrime (table indices of the unit lists)
+};
+// Ranges per launch: several chunks of one device (dse_sieve_all with P >
+// devices, and the dropped tail) go to one persistent launch, so no chunk's
+// partial last round of segments leaves the CUs idle and no host launch
+// latency sits between chunks.
+constexpr uint32_t kMaxRanges = 9;
+
+struct WheelArgs {
+  WheelRange r[kMaxRanges];
+  uint32_t nranges;    // 1..kMaxRanges (1 with bucketed primes)
+  uint32_t nseg;       // segments of all ranges
+  uint32_t nthr[5];    // odd primes <= 61, TA, TB1, TB, kWheelMaxPrime (table indices of the unit lists)
   // Bucketed hits of the primes > kWheelMaxPrime (bk_start null: none), as
   // entries (bucket_entry):
   const uint32_t* bk_entries;  // band 1: segment s owns [bk_start[s], bk_start[s+1])
@@ -170,78 +199,66 @@ __device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint32_t*)p;
 }
 
-// Mark period `off` of the column whose word 0 is at LDS byte address `cb`:
-// images are 64 KiB aligned and a column's byte offset is < 256, so the row
-// offset (off >> 5) * 256 (< 64 KiB) and the column combine with one v_and_or.
-// Issued as asm: callers drain lgkmcnt before a barrier (lds_drain), since the
-// compiler's waitcnt pass does not see it.
-__device__ __forceinline__ void mark_col(uint32_t cb, uint32_t off, uint32_t one) {
-  uint32_t a, b;
-  asm volatile(
-      "v_lshlrev_b32 %0, 3, %2\n\t"
-      "v_and_or_b32 %0, %0, %4, %3\n\t"
-      "v_lshlrev_b32 %1, %2, %5\n\t"
-      "ds_or_b32 %0, %1"
-      : "=&v"(a), "=&v"(b)
-      : "v"(off), "v"(cb), "s"(0xffffff00u), "v"(one)
-      : "memory");
-}
-
-// 1 << (x & 31) as a 4-byte VOP2 (the shifted 1 in a VGPR: with the inline
-// constant in the value operand the instruction needs the 8-byte VOP3 form,
-// and the wheel kernel is bound by instruction fetch)
-__device__ __forceinline__ uint32_t shl1(uint32_t x, uint32_t one) {
-  uint32_t r;
-  asm("v_lshlrev_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(one));
-  return r;
-}
-
+// Every mark is issued as asm: the compiler's waitcnt pass does not see it,
+// so callers drain lgkmcnt before a barrier (lds_drain); and it does not
+// unroll loops around it, so runs are unrolled by hand.
 __device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// Keeps a marking offset opaque to loop strength reduction, which otherwise
-// splits it into several induction variables (7 VALU per mark instead of 4).
+// Keeps a value opaque to the optimiser (loop strength reduction splits a
+// marking offset into several induction variables; lane-derived constants get
+// hoisted out of the segment loop and spilled).
 __device__ __forceinline__ uint32_t opaque(uint32_t x) {
   asm volatile("" : "+v"(x));
   return x;
 }
 
-// Mark period `off` of the column at cb and advance off by p, in one asm
-// block (written as mark_col + an add, the loop-carried offset costs a
-// v_mov per mark).
-__device__ __forceinline__ void mark_col_step(uint32_t cb, uint32_t& off, uint32_t p, uint32_t one) {
+constexpr uint32_t kBlockMask = ~31u;  // period index -> its block's byte address
+
+// Mark period k (< KP) of the plane whose byte base is pb4 (image + 4 plane):
+// address (k & ~31) | pb4 in one v_and_or, bit 1 << (k & 31) (the shift reads
+// the low 5 bits itself). 2 VALU.
+__device__ __forceinline__ void mark_k(uint32_t pb4, uint32_t k, uint32_t one) {
   uint32_t a, b;
   asm volatile(
-      "v_lshlrev_b32 %0, 3, %2\n\t"
-      "v_and_or_b32 %0, %0, %4, %3\n\t"
-      "v_lshlrev_b32 %1, %2, %6\n\t"
-      "ds_or_b32 %0, %1\n\t"
-      "v_add_u32 %2, %2, %5"
-      : "=&v"(a), "=&v"(b), "+v"(off)
-      : "v"(cb), "s"(0xffffff00u), "v"(p), "v"(one)
+      "v_and_or_b32 %0, %2, %3, %4\n\t"
+      "v_lshlrev_b32 %1, %2, %5\n\t"
+      "ds_or_b32 %0, %1"
+      : "=&v"(a), "=&v"(b)
+      : "v"(k), "s"(kBlockMask), "v"(pb4), "v"(one)
       : "memory");
 }
 
-// n unconditional marks off, off + p, ... in one column, unrolled by 4 by
-// hand (the asm marks keep the compiler from unrolling, which costs three
-// SALU of loop control per mark); returns the offset after the run.
-__device__ __forceinline__ uint32_t mark_run(uint32_t cb, uint32_t off, uint32_t p, uint32_t n, uint32_t one) {
-  uint32_t h = 0;
-  for (; h + 4 <= n; h += 4) {
-    mark_col_step(cb, off, p, one);
-    mark_col_step(cb, off, p, one);
-    mark_col_step(cb, off, p, one);
-    mark_col_step(cb, off, p, one);
-  }
-  for (; h < n; ++h) mark_col_step(cb, off, p, one);
-  return off;
+// mark_k and advance k by p, in one asm block (written as mark_k + an add,
+// the loop-carried index costs a v_mov per mark). 3 VALU.
+__device__ __forceinline__ void mark_k_step(uint32_t pb4, uint32_t& k, uint32_t p, uint32_t one) {
+  uint32_t a, b;
+  asm volatile(
+      "v_and_or_b32 %0, %2, %3, %4\n\t"
+      "v_lshlrev_b32 %1, %2, %6\n\t"
+      "ds_or_b32 %0, %1\n\t"
+      "v_add_u32 %2, %2, %5"
+      : "=&v"(a), "=&v"(b), "+v"(k)
+      : "s"(kBlockMask), "v"(pb4), "v"(p), "v"(one)
+      : "memory");
 }
 
-// Mark period `off` of the column at byte address cb if off < LS; returns the
-// offset of the next hit. A lane without the hit leaves the ds_or (exec mask:
-// no bit select, and idle lanes take no part in bank conflicts).
-__device__ __forceinline__ uint32_t mark_col_pred(uint32_t cb, uint32_t off, uint32_t p, uint32_t one) {
-  if (off < LS) mark_col_step(cb, off, p, one);
-  return off;
+// n unconditional marks k, k + p, ... (unrolled by 4 by hand: three SALU of
+// loop control per mark otherwise); returns the index after the run.
+__device__ __forceinline__ uint32_t mark_run(uint32_t pb4, uint32_t k, uint32_t p, uint32_t n, uint32_t one) {
+  uint32_t h = 0;
+  for (; h + 4 <= n; h += 4) {
+    mark_k_step(pb4, k, p, one);
+    mark_k_step(pb4, k, p, one);
+    mark_k_step(pb4, k, p, one);
+    mark_k_step(pb4, k, p, one);
+  }
+  for (; h < n; ++h) mark_k_step(pb4, k, p, one);
+  return k;
+}
+
+// ds_or_b32 at a precomputed LDS byte address.
+__device__ __forceinline__ void mark_at(uint32_t a, uint32_t bit) {
+  asm volatile("ds_or_b32 %0, %1" : : "v"(a), "v"(bit) : "memory");
 }
 
 // x mod p for x < 2^63 with m = floor((2^64-1)/p).
@@ -258,16 +275,6 @@ __host__ __device__ __forceinline__ uint32_t mod_barrett(uint64_t x, uint32_t p,
 }
 
 __device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
-
-
-// t mod p, t < 2^24
-__device__ __forceinline__ uint32_t mod_small(uint32_t t, uint32_t p, float invp) {
-  uint32_t q = (uint32_t)((float)t * invp);
-  int32_t r = (int32_t)(t - q * p);
-  r = r < 0 ? r + (int32_t)p : r;
-  r = r >= (int32_t)p ? r - (int32_t)p : r;
-  return (uint32_t)r;
-}
 
 // ceil(t / p), t < 2^24
 __device__ __forceinline__ uint32_t div_ceil_small(uint32_t t, uint32_t p, float invp) {
@@ -327,29 +334,6 @@ __device__ __forceinline__ uint32_t kmin_for(uint32_t D, uint32_t rho) {
   return D > rho ? (D - rho + 29u) / 30u : 0u;
 }
 
-// 8 diagonal column steps of one lane's prime: per column n_u unconditional
-// marks and NX (template; NX < 0: n_x at run time) value-predicated ones
-// (wave-uniform counts, so the loop control runs on the scalar unit); at the
-// wrap from column 7 back to column 0 the offset restarts at the plane start O0.
-// pb = LDS byte address of the plane's word in column 0 (image + 4 * plane).
-template <int NX>
-__device__ __forceinline__ void diag_walk(uint32_t off, uint32_t p, uint32_t pb, uint32_t c, uint32_t O0,
-                                          uint32_t n_u, uint32_t n_x, uint32_t one) {
-  for (uint32_t t = 0; t < 8; ++t) {
-    const uint32_t cb_col = pb + 32 * c;
-    off = mark_run(cb_col, off, p, n_u, one);
-    if (NX >= 0) {
-#pragma unroll
-      for (int h = 0; h < NX; ++h) off = mark_col_pred(cb_col, off, p, one);
-    } else {
-      for (uint32_t h = 0; h < n_x; ++h) off = mark_col_pred(cb_col, off, p, one);
-    }
-    off -= LS;
-    c = (c + 1) & 7;
-    off = c == 0 ? O0 : off;
-  }
-}
-
 // (x & m) | (y & ~m): v_bfi_b32
 // (the compiler rewrites the C form into v_and + v_bitop3 pairs)
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t x, uint32_t y) {
@@ -381,50 +365,40 @@ __device__ __forceinline__ void bit_block_swaps(uint32_t (&W)[8]) {
 
 // ---- work units of the mark phase ----------------------------------------
 
-// ds_or_b32 at a precomputed LDS byte address (asm: see mark_col).
-__device__ __forceinline__ void mark_at(uint32_t a, uint32_t bit) {
-  asm volatile("ds_or_b32 %0, %1" : : "v"(a), "v"(bit) : "memory");
-}
-
-// A primes below TA_CLS, one column per lane, by residue class of the hit
-// index mod 32: hits n0, n0 + 32, n0 + 64, ... of a column share their bit
-// and sit p rows apart, so after 4 VALU of class setup each further mark is
-// one v_add of the wave-uniform 256 p (instead of 4 VALU per mark). Every
-// class has K = ROWS / p or K + 1 hits (its first row is < p): K marks, then
-// one predicated by row < ROWS (exec mask). off = first hit in the column
-// (< p), img0 = image base (aligned to the image size).
-#ifndef DSE_TA_CLS
-#define DSE_TA_CLS 224
-#endif
-constexpr uint32_t TA_CLS = DSE_TA_CLS;
-constexpr uint32_t IMG_BYTES = IMG_WORDS * 4;
-static_assert((IMG_BYTES & (IMG_BYTES - 1)) == 0, "image size is a power of two");
+// A, by hit class: lane (plane, c) owns the hits n of its plane with n mod
+// 256 = 32c + r, r = 0..31; class r's hits k0 + 256p t share their bit and
+// their byte addresses step by the wave-uniform 256p, so after 3 VALU of class
+// setup each further mark is one v_add. k0 = kp + (32c + r) p < 256p, so
+// every class has K = floor(KP / 256p) or K + 1 hits: K marks, then one
+// predicated by address < IMG_BYTES (exec mask). k = the class-0 hit of the
+// lane; the image is at LDS address 0.
 template <int K>
-__device__ __forceinline__ void a_classes(uint32_t img0, uint32_t cb_col, uint32_t off, uint32_t p, uint32_t one) {
-  const uint32_t D = p << 8;  // p rows
+__device__ __forceinline__ void a_classes(uint32_t pb4, uint32_t k, uint32_t p, uint32_t one) {
+  const uint32_t D = p << 8;  // 256 p periods = bytes
 #pragma unroll 1
-  for (uint32_t n0 = 0; n0 < 32; ++n0) {
+  for (uint32_t r = 0; r < 32; ++r) {
     uint32_t a, bit;
     asm volatile(
-        "v_lshlrev_b32 %0, 3, %2\n\t"
-        "v_and_or_b32 %0, %0, %3, %4\n\t"
+        "v_and_or_b32 %0, %2, %3, %4\n\t"
         "v_lshlrev_b32 %1, %2, %5"
         : "=&v"(a), "=&v"(bit)
-        : "v"(off), "s"(0xffffff00u), "v"(cb_col), "v"(one));
+        : "v"(k), "s"(kBlockMask), "v"(pb4), "v"(one));
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
+    for (int t = 0; t < K; ++t) {
       mark_at(a, bit);
       a += D;
     }
-    if (a < img0 + IMG_BYTES) mark_at(a, bit);  // exec mask, as mark_col_pred
-    off = opaque(off + p);
+    if (a < IMG_BYTES) mark_at(a, bit);
+    k = opaque(k + p);
   }
 }
 
-// A: one mid prime (61 < p <= TA) per wave; lane L walks column L =
-// (plane L&7, column L>>3).
-__device__ __forceinline__ void unit_A(uint32_t* __restrict__ img, uint32_t pi, uint64_t m, uint64_t Vs,
-                                       uint64_t rho_pack, uint32_t lane, uint32_t one) {
+// A: one mid prime (61 < p <= TA) per wave; lane (plane L & 7, c = L >> 3).
+// Lanes 0-31 have c = 0..3: a plane's four lanes mark 32p periods apart at
+// every step (same class r, same t), i.e. in blocks c p (mod 4) apart -- four
+// distinct banks for odd p.
+__device__ __forceinline__ void unit_A(uint32_t img0, uint32_t pi, uint64_t m, uint64_t Vs, uint64_t rho_pack,
+                                       uint32_t lane, uint32_t one) {
   const uint32_t p = pi & 0xFFFFu, inv30 = pi >> 16;  // wave-uniform
   const uint64_t p2 = (uint64_t)p * p;
   const uint32_t Xs = mod_barrett(Vs, p, m);            // scalar unit
@@ -432,40 +406,80 @@ __device__ __forceinline__ void unit_A(uint32_t* __restrict__ img, uint32_t pi, 
   const uint32_t pl = lane & 7, c = lane >> 3;
   const uint32_t rho = (uint32_t)(rho_pack >> (5 * pl)) & 31u;
   const uint32_t kp = plane_first(Xs, rho, p, inv30, invp);
-  const uint32_t cb_col = lds_addr(img) + 4 * lane;
+  const uint32_t pb4 = img0 + 4 * pl;
+  const uint32_t k = kp + 32 * c * p;                   // class 0 of the lane: hit n = 32c
   if (p2 <= Vs) {
-    const uint32_t cm = mod_small(c * LS, p, invp);
-    uint32_t off = kp >= cm ? kp - cm : kp + p - cm;
-    const uint32_t K = ROWS / p;  // wave-uniform, scalar
-    if (p < TA_CLS) {
-      switch (K) {  // ROWS / p for 61 < p < TA_CLS
-        case 2: a_classes<2>(lds_addr(img), cb_col, off, p, one); return;
-        case 3: a_classes<3>(lds_addr(img), cb_col, off, p, one); return;
-        case 4: a_classes<4>(lds_addr(img), cb_col, off, p, one); return;
-        case 5: a_classes<5>(lds_addr(img), cb_col, off, p, one); return;
-        case 6: a_classes<6>(lds_addr(img), cb_col, off, p, one); return;
-        case 7: a_classes<7>(lds_addr(img), cb_col, off, p, one); return;
-        default: break;
-      }
+    switch (KP / (256 * p)) {  // K (wave-uniform): 2..7 for 61 < p <= 256 (1..4 for the half geometry)
+      case 1: a_classes<1>(pb4, k, p, one); return;
+      case 2: a_classes<2>(pb4, k, p, one); return;
+      case 3: a_classes<3>(pb4, k, p, one); return;
+      case 4: a_classes<4>(pb4, k, p, one); return;
+      case 5: a_classes<5>(pb4, k, p, one); return;
+      case 6: a_classes<6>(pb4, k, p, one); return;
+      case 7: a_classes<7>(pb4, k, p, one); return;
+      default: __builtin_unreachable();
     }
-    const uint32_t n_full = div_small(LS, p, invp);
-    off = mark_run(cb_col, off, p, n_full, one);
-    if (off < LS) mark_col(cb_col, off, one);
-  } else {
-    const uint32_t kmin = kmin_for((uint32_t)(p2 - Vs), rho);
-    const uint32_t kf = first_at_or_after(kp, max(kmin, c * LS), p, invp);
-    for (uint32_t off = kf - c * LS; off < LS; off += p) mark_col(cb_col, off, one);
+  }
+  // p^2 inside the segment (its first segments only): the lane's hits with
+  // k >= kmin, one at a time
+  const uint32_t kmin = kmin_for((uint32_t)(p2 - Vs), rho);
+  for (uint32_t r = 0; r < 32; ++r)
+    for (uint32_t kk = k + r * p; kk < KP; kk += 256 * p)
+      if (kk >= kmin) mark_k(pb4, kk, one);
+}
+
+// B1: two mid primes (TA < p <= TB1), one per half-wave; lane (plane L & 7,
+// j = (L >> 3) & 3) owns the hits n with n mod 128 in [32j, 32j + 32), in
+// order: 32 marks k, k + p, ... then a jump of 96p. The four lanes of a plane
+// are 32p periods apart: distinct banks, as in A. Blocks of 128 hits every
+// lane fills are unrolled without a test; the last one, partly filled, is
+// marked with a per-lane count.
+__device__ __forceinline__ void unit_B1(uint32_t img0, const uint32_t* __restrict__ s_mid_p,
+                                        const uint64_t* __restrict__ s_mid_m, uint32_t j0, uint32_t nj, uint64_t Vs,
+                                        uint64_t rho_pack, uint32_t lane, uint32_t one) {
+  const uint32_t h = lane >> 5, pl = lane & 7, j = (lane >> 3) & 3;
+  if (h >= nj) return;  // the unit's second half-wave when the list ends
+  const uint32_t pi = s_mid_p[j0 + h];
+  const uint32_t p = pi & 0xFFFFu, inv30 = pi >> 16;
+  const uint64_t m = s_mid_m[j0 + h];
+  const float invp = fast_rcp((float)p);
+  const uint32_t rho = (uint32_t)(rho_pack >> (5 * pl)) & 31u;
+  const uint32_t kp = plane_first(mod_barrett(Vs, p, m), rho, p, inv30, invp);
+  const uint32_t pb4 = img0 + 4 * pl;
+  uint32_t k = kp + 32 * j * p;                          // hit n = 32j
+  const uint64_t p2 = (uint64_t)p * p;
+  if (p2 > Vs) {  // p^2 inside the segment: one at a time from kmin
+    const uint32_t kmin = kmin_for((uint32_t)min(p2 - Vs, (uint64_t)0xFFFFFFFFu), rho);
+    for (; k < KP; k += 96 * p)
+      for (uint32_t r = 0; r < 32 && k < KP; ++r, k += p)
+        if (k >= kmin) mark_k(pb4, k, one);
+    return;
+  }
+  // blocks every lane of the wave fills: n < 128 (t + 1) <= floor(KP / pmax)
+  const uint32_t pmax = __builtin_amdgcn_readlane(p, nj == 2 ? 32 : 0);  // the list ascends
+  const uint32_t tf = (KP / pmax) / 128;  // wave-uniform (a scalar division)
+  const uint32_t skip = 96 * p;
+#pragma unroll 1
+  for (uint32_t t = 0; t < tf; ++t) {
+    k = mark_run(pb4, k, p, 32, one);
+    k += skip;
+  }
+  // the rest: ceil((KP - k) / p) hits left in this lane's next blocks of 32
+  while (k < KP) {
+    const uint32_t left = div_ceil_small(KP - k, p, invp);
+    const uint32_t n = min(left, 32u);
+    for (uint32_t r = 0; r < n; ++r) mark_k_step(pb4, k, p, one);
+    k += skip;
   }
 }
 
-// B: 8 mid primes (TA < p <= LS) x 8 planes; lane (prime jp, plane pl)
-// walks columns jp, jp+1, ... (mod 8). Half-wave g holds primes 4g..4g+3, so
-// at every step its lanes are in 4 consecutive columns c (distinct c mod 4) x
-// 8 planes: 32 distinct banks 8 (c mod 4) + pl.
-__device__ __forceinline__ void unit_B(uint32_t* __restrict__ img, const uint32_t* __restrict__ s_mid_p,
-                                       const uint64_t* __restrict__ s_mid_m, uint32_t j0, uint32_t nj, uint64_t Vs,
-                                       uint64_t Vend, uint64_t rho_pack, uint32_t lane, uint32_t one) {
-  const uint32_t pfirst = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
+// B2: 8 mid primes (TB1 < p <= TB) x 8 planes; lane (prime L >> 3, plane
+// L & 7) walks its plane's hits in order: n_u unconditional marks for every
+// lane, then a short per-lane tail. A plane's lanes hold different primes,
+// so their banks collide at random (the L pattern).
+__device__ __forceinline__ void unit_B2(uint32_t img0, const uint32_t* __restrict__ s_mid_p,
+                                        const uint64_t* __restrict__ s_mid_m, uint32_t j0, uint32_t nj, uint64_t Vs,
+                                        uint64_t Vend, uint64_t rho_pack, uint32_t lane, uint32_t one) {
   const uint32_t pl = lane & 7, jp = lane >> 3;
   const bool valid = jp < nj;
   const uint32_t pi = s_mid_p[valid ? j0 + jp : j0];
@@ -473,33 +487,19 @@ __device__ __forceinline__ void unit_B(uint32_t* __restrict__ img, const uint32_
   const uint64_t m = s_mid_m[valid ? j0 + jp : j0];
   const float invp = fast_rcp((float)p);
   const uint32_t rho = (uint32_t)(rho_pack >> (5 * pl)) & 31u;
-  const uint32_t Xs = mod_barrett(Vs, p, m);
-  const uint32_t kp = plane_first(Xs, rho, p, inv30, invp);
+  uint32_t k = plane_first(mod_barrett(Vs, p, m), rho, p, inv30, invp);
   const uint64_t p2 = (uint64_t)p * p;
-  uint32_t O0, off;
-  const uint32_t cstart = jp * LS;
   const bool slow = p2 > Vs;
-  if (!slow) {
-    O0 = kp;
-    const uint32_t cm = mod_small(cstart, p, invp);
-    off = kp >= cm ? kp - cm : kp + p - cm;
-  } else {
-    const uint32_t kmin = p2 >= Vend ? KP : kmin_for((uint32_t)(p2 - Vs), rho);
-    O0 = first_at_or_after(kp, kmin, p, invp);
-    off = first_at_or_after(kp, max(kmin, cstart), p, invp) - cstart;
-  }
-  const uint32_t pmin = pfirst;
+  if (slow) k = p2 >= Vend ? KP : first_at_or_after(k, kmin_for((uint32_t)(p2 - Vs), rho), p, invp);
   const uint32_t pmax = __builtin_amdgcn_readfirstlane(s_mid_p[j0 + nj - 1]) & 0xFFFFu;
   const bool any_slow = __builtin_amdgcn_ballot_w64(slow) != 0;
-  const uint32_t n_u = any_slow ? 0u : div_small(LS, pmax, fast_rcp((float)pmax));
-  const uint32_t n_x = div_ceil_small(LS, pmin, fast_rcp((float)pmin)) - n_u;
-  const uint32_t pb = lds_addr(img) + 4 * pl;
+  const uint32_t n_u = any_slow ? 0u : KP / pmax;  // every lane has >= floor(KP / p) of them (k < p)
+  const uint32_t pb4 = img0 + 4 * pl;
   // lanes past the batch end mark nothing (their unconditional marks would
-  // land in another prime's columns)
+  // land in another prime's plane)
   if (!valid) return;
-  if (n_x == 1) diag_walk<1>(off, p, pb, jp, O0, n_u, 1, one);
-  else if (n_x == 2) diag_walk<2>(off, p, pb, jp, O0, n_u, 2, one);
-  else diag_walk<-1>(off, p, pb, jp, O0, n_u, n_x, one);
+  k = mark_run(pb4, k, p, n_u, one);
+  for (; k < KP; k += p) mark_k(pb4, k, one);
 }
 
 // Operands of one large unit, loaded ahead of use. The table row of prime i
@@ -522,32 +522,19 @@ __device__ __forceinline__ void load_L(LargeOps& o, const uint32_t* __restrict__
   o.a[4] = hi.x; o.a[5] = hi.y; o.a[6] = hi.z; o.a[7] = hi.w;
 }
 
-// Mark plane-relative period kk of plane byte base pb4 = image + 4 * plane:
-// word (row (kk >> 5) & (ROWS-1), column 8 * (kk >> LOG_LS) + plane). PRED:
-// only if kk < KP -- a lane without a hit leaves the ds_or (exec mask), so it
-// adds no bank conflict (an OR of 0 at a random column conflicts like a
-// mark). asm for the same reason as mark_col.
+// Mark plane-relative period kk of plane byte base pb4 = image + 4 * plane
+// (mark_k: 2 VALU). PRED: only if kk < KP -- a lane without a hit leaves the
+// ds_or (exec mask), so it adds no bank conflict (an OR of 0 at a random
+// block conflicts like a mark).
 template <bool PRED>
 __device__ __forceinline__ void mark_plane(uint32_t pb4, uint32_t kk, uint32_t one) {
   if (PRED && kk >= KP) return;
-  // kk < KP wherever the mark is executed: the column is kk >> LOG_LS (a
-  // 4-byte shift, not an 8-byte bfe)
-  const uint32_t col = kk >> LOG_LS;
-  const uint32_t bit = shl1(kk, one);
-  uint32_t a, t;
-  asm volatile(
-      "v_lshl_or_b32 %1, %2, 5, %3\n\t"
-      "v_lshlrev_b32 %0, 3, %4\n\t"
-      "v_and_or_b32 %0, %0, %5, %1\n\t"
-      "ds_or_b32 %0, %6"
-      : "=&v"(a), "=&v"(t)
-      : "v"(col), "v"(pb4), "v"(kk), "s"((ROWS - 1) << 8), "v"(bit)
-      : "memory");
+  mark_k(pb4, kk, one);
 }
 
 // Mark a bucketed hit: entry = LDS word index << 5 | bit (bucket_entry), so
-// the address is img0 + (e >> 5) * 4 and the bit 1 << (e & 31) (the shift reads the
-// low 5 bits itself): 3 VALU, where a (k, plane) entry took 8.
+// the address is img0 + (e >> 5) * 4 and the bit 1 << (e & 31) (the shift
+// reads the low 5 bits itself): 3 VALU.
 __device__ __forceinline__ void mark_entry(uint32_t img0, uint32_t e, uint32_t one) {
   uint32_t a, b;
   asm volatile(
@@ -603,16 +590,7 @@ __device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, co
       mark_plane<true>(pb4, kk, ps.one);
       mark_plane<true>(pb4, kk + p, ps.one);
     } else {
-      uint32_t h = 0;
-      for (; h + 2 <= n_min; h += 2) {  // unrolled by hand (asm marks)
-        mark_plane<false>(pb4, kk, ps.one);
-        mark_plane<false>(pb4, opaque(kk + p), ps.one);
-        kk = opaque(kk + 2 * p);
-      }
-      if (h < n_min) {
-        mark_plane<false>(pb4, kk, ps.one);
-        kk = opaque(kk + p);
-      }
+      kk = mark_run(pb4, kk, p, n_min, ps.one);
       for (; kk < KP; kk += p) mark_plane<false>(pb4, kk, ps.one);  // a predicated fixed-count tail is slower
     }
   }
@@ -691,26 +669,24 @@ struct WheelLds {
   uint32_t img[IMG_WORDS];         // the segment image, at LDS address 0
   uint64_t mid_m[kMidCap];         // Barrett factors of the staged mid primes
   uint32_t mid_p[kMidCap];         // p | (30^{-1} mod p) << 16
-  uint32_t lut[256];               // period byte -> 15 odd slots
+  uint32_t lut[kMaxRanges][256];   // per range: period byte -> 15 odd slots
   uint4 itab[kGDW];                // init tables U_G, 4 copies shifted by 0..3 dwords (kGDW / 4 blocks each)
-  uint32_t thr[4];
+  uint32_t thr[5];
   uint32_t ctr;                    // unit counter
-  unsigned long long wave_cnt[NW];
+  unsigned long long rcnt[kMaxRanges];  // per range: primes counted by this workgroup
 };
 
 // BK: the range has bucketed primes (wa.bk_*). Two instantiations, so the
 // ranges without (N up to 1.1e12) run a unit loop without the bucket code
 // (with it, the loop's SGPR spills doubled and 1e11 ran 1.9% slower).
 template <bool BK>
-__global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restrict__ table, WheelArgs wa,
-                                                            uint32_t* __restrict__ out,
-                                                            unsigned long long* __restrict__ count_out) {
-  // One static LDS object, so the images sit at LDS addresses 0 and 64 KiB
-  // (mark_col / mark_plane combine row and column offsets with a bitwise or).
+__global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restrict__ table, WheelArgs wa) {
+  // One static LDS object, so the image sits at LDS address 0 (mark_k and
+  // a_classes combine a block's byte address and a plane with a bitwise or,
+  // and bound it by IMG_BYTES).
   __shared__ WheelLds lds;
   uint64_t* const s_mid_m = lds.mid_m;
   uint32_t* const s_mid_p = lds.mid_p;
-  uint32_t* const s_lut = lds.lut;
   uint32_t* const s_thr = lds.thr;
 
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
@@ -724,68 +700,82 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   const uint32_t tid = threadIdx.x, lane_id = tid & 63, wave = tid >> 6;
 
   if (tid == 0) {
-    // first index with p > 61, with p > TA, with p > TB (capped by the LDS
-    // stage), with p > kWheelMaxPrime (bucketed or absent): the table holds
-    // every odd prime from 3 up, so these are the host's prime counts
-    // (wa.nthr), capped by the table's size
+    // first index with p > 61, > TA, > TB1, > TB (capped by the LDS stage),
+    // > kWheelMaxPrime (bucketed or absent): the table holds every odd prime
+    // from 3 up, so these are the host's prime counts (wa.nthr), capped by
+    // the table's size
     s_thr[0] = min(wa.nthr[0], np);
     s_thr[1] = min(wa.nthr[1], np);
-    s_thr[2] = min(min(wa.nthr[2], np), s_thr[0] + kMidCap);
-    s_thr[3] = max(s_thr[2], min(wa.nthr[3], np));
+    s_thr[2] = min(wa.nthr[2], np);
+    s_thr[3] = min(min(wa.nthr[3], np), s_thr[0] + kMidCap);
+    s_thr[2] = min(s_thr[2], s_thr[3]);
+    s_thr[4] = max(s_thr[3], min(wa.nthr[4], np));
     lds.ctr = 0;
   }
-  if (tid < 256) {
+  if (tid < kMaxRanges) lds.rcnt[tid] = 0;
+  for (uint32_t x = tid; x < 256 * wa.nranges; x += NT) {
+    const uint32_t v8 = x & 255;
+    const uint64_t rho_pack = wa.r[x >> 8].rho_pack;
     uint32_t v = 0;
 #pragma unroll
     for (uint32_t i = 0; i < 8; ++i) {
-      const uint32_t rho = (uint32_t)(wa.rho_pack >> (5 * i)) & 31u;
-      if (!(tid & (1u << i))) v |= 1u << ((rho - 1) >> 1);  // plane bit i clear: prime
+      const uint32_t rho = (uint32_t)(rho_pack >> (5 * i)) & 31u;
+      if (!(v8 & (1u << i))) v |= 1u << ((rho - 1) >> 1);  // plane bit i clear: prime
     }
     // composite bits of the 8 planes -> prime odd slots of the period, filed
-    // under lut_index(tid) (see there)
-    s_lut[tid ^ (3u * (tid >> 5))] = v;
+    // under v ^ 3 (v >> 5) (see expand_segment)
+    lds.lut[x >> 8][v8 ^ (3u * (v8 >> 5))] = v;
   }
   for (uint32_t idx = tid; idx < 4 * kGDW; idx += NT) reinterpret_cast<uint32_t*>(lds.itab)[idx] = g_init_tables.w[idx];
   __syncthreads();
-  const uint32_t i_mid0 = s_thr[0], i_midB = s_thr[1], i_mid1 = s_thr[2];
+  const uint32_t i_mid0 = s_thr[0], i_midB = s_thr[1], i_midB2 = s_thr[2], i_mid1 = s_thr[3];
   for (uint32_t i = tid; i < i_mid1 - i_mid0; i += NT) {
     const uint32_t q = P[i_mid0 + i];
     s_mid_p[i] = q | ((uint32_t)inv30_of(q) << 16);  // p < 2^14, 30^{-1} mod p < p
     s_mid_m[i] = M[i_mid0 + i];
   }
-  // Work units: list 1 = nA single mid primes, then nB diagonal units (8
-  // primes each); list 2 = nL large units (two sets of 64 primes each); handed
-  // out through one dynamic queue. Issue arbitration favours older waves, so
-  // any static split finishes the youngest waves last; the queue makes them
-  // take fewer units instead.
+  // Work units: list 1 = nA single mid primes (A), nB1 units of two primes
+  // (B1), nB2 units of 8 primes (B2); list 2 = nL large units (two sets of 64
+  // primes each); handed out through one dynamic queue. Issue arbitration
+  // favours older waves, so any static split finishes the youngest waves
+  // last; the queue makes them take fewer units instead.
   const uint32_t nA = i_midB - i_mid0;
   const uint32_t n_mid = i_mid1 - i_mid0;
-  const uint32_t nB = (i_mid1 - i_midB + 7) / 8;
-  const uint32_t i_big = s_thr[3];             // L units end here
+  const uint32_t n_b1 = i_midB2 - i_mid0;      // staged index where B2 starts
+  const uint32_t nB1 = (i_midB2 - i_midB + 1) / 2;
+  const uint32_t nB2 = (i_mid1 - i_midB2 + 7) / 8;
+  const uint32_t i_big = s_thr[4];             // L units end here
   constexpr uint32_t kLU = 128;                // primes per L unit
   const uint32_t nL = (i_big - i_mid1 + kLU - 1) / kLU;
-  const uint32_t n1 = nA + nB, n2 = nL;
+  const uint32_t n1 = nA + nB1 + nB2, n2 = nL;
 
-  const uint64_t out_words = 2ull * ((wa.nbits + 63) / 64);  // 32-bit words of the caller's mask
-  const uint64_t nseg = (wa.nbits + kWheelOutBits - 1) / kWheelOutBits;
-  const uint64_t grid = gridDim.x;
-  const uint32_t T = blockIdx.x < nseg ? (uint32_t)((nseg - 1 - blockIdx.x) / grid + 1) : 0u;  // rounds
-  unsigned long long my_count = 0;
+  const uint32_t nseg = wa.nseg;
+  const uint32_t grid = gridDim.x;
+  const uint32_t T = blockIdx.x < nseg ? (nseg - 1 - blockIdx.x) / grid + 1 : 0u;  // rounds
+  // launch segment g -> its range (uniform: a scan of <= kMaxRanges starts)
+  auto range_of = [&](uint32_t g) -> uint32_t {
+    uint32_t r = 0;
+    for (uint32_t i = 1; i < wa.nranges; ++i) r = g >= wa.r[i].seg0 ? i : r;
+    return r;
+  };
 
-  // ---- init: small-prime patterns (7..61) of segment s into the image.
-  // Wave w writes rows w*ROWS/NW .. +ROWS/NW of every column: the rows it
-  // expands, so it may init the image right after expanding it.
-  auto init_segment = [&](uint32_t* __restrict__ img, uint64_t s) {
+  // ---- init: small-prime patterns (7..61) of segment s into the image. Lane
+  // (plane L & 7, run q = 8 w + (L >> 3)) of wave w writes its plane's words
+  // of the kInitWords consecutive blocks [kInitWords q, +kInitWords): the
+  // blocks this wave expands, so it may init them right after expanding.
+  auto init_segment = [&](uint32_t* __restrict__ img, uint32_t g_seg) {
+    const WheelRange& rg = wa.r[range_of(g_seg)];
+    const uint64_t s = g_seg - rg.seg0;  // the range's segment
     uint32_t lane = lane_id;
     asm volatile("" : "+v"(lane));
-    const uint32_t C = lane, pl = lane & 7, c = lane >> 3;
-    const uint32_t rho = (uint32_t)(wa.rho_pack >> (5 * pl)) & 31u;
-    const uint32_t r0 = wave * (ROWS / NW);
-    const uint32_t k0 = c * LS + 32 * r0;                // first period of the lane's words
-    constexpr uint32_t R = ROWS / NW;  // words per lane
-    constexpr uint32_t H = 16;         // words per pass (bounds the registers: 16 acc + 20 read)
+    const uint32_t pl = lane & 7, q = 8 * wave + (lane >> 3);
+    const uint32_t rho = (uint32_t)(rg.rho_pack >> (5 * pl)) & 31u;
+    constexpr uint32_t R = kInitWords;  // words per lane
+    const uint32_t b0 = R * q;          // first block of the run
+    const uint32_t k0 = 32 * b0;        // its first period
+    constexpr uint32_t H = 16;          // words per pass (bounds the registers: 16 acc + 20 read)
     static_assert(R % H == 0 && H % 4 == 0, "init passes");
-    uint32_t boff[kNG], bsh[kNG];      // per group: the lane's first aligned 16-byte block, bit shift
+    uint32_t boff[kNG], bsh[kNG];       // per group: the lane's first aligned 16-byte block, bit shift
     // rho takes 8 values over the lanes: left visible, the compiler evaluates
     // the group offsets for all 8 on the scalar unit and selects per lane
     // (a 6.8x SALU blow-up, 33 ms kernels); opaque, it is one VALU chain.
@@ -795,12 +785,13 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       const uint32_t Mg = gmod(g);
       const uint32_t wg = (uint32_t)(kWheelSpan % Mg);
       const uint32_t sg = (uint32_t)(s % Mg);
-      const uint32_t x = ((uint32_t)wa.v0g[g] + sg * wg + rho_o) % Mg;  // (Vs + rho) mod M_G
+      const uint32_t x = ((uint32_t)rg.v0g[g] + sg * wg + rho_o) % Mg;  // (Vs + rho) mod M_G
       const uint32_t o = (k0_o + x * kGInv30[g]) % Mg;                  // bit offset of period k0
       const uint32_t d0 = o >> 5, kc = d0 & 3;
       boff[g] = (kc * kGDW + gbase(g) + d0 - kc) / 4;                    // 16-byte block index
       bsh[g] = o & 31;
     }
+    uint32_t* const wp = img + 8 * b0 + pl;
 #pragma unroll
     for (uint32_t h = 0; h < R; h += H) {
       uint32_t acc[H];
@@ -820,33 +811,41 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         asm volatile("" ::: "memory");  // keep the next group's reads after these (register pressure)
       }
 #pragma unroll
-      for (uint32_t r = 0; r < H; ++r) img[(r0 + h + r) * 64 + C] = acc[r];
+      for (uint32_t r = 0; r < H; ++r) wp[8 * (h + r)] = acc[r];
     }
   };
 
-  // ---- expand segment s (image img) to odd-only bits, count, store: lane
-  // (column c, row) of wave w reads that row of column c in all 8 planes (32
-  // contiguous bytes, two ds_read_b128), rows
-  // 8 * (ROWS/(8 NW) * w + t) + ro. ds_read_b128 serves a wave in 4 lane
-  // groups of 16 ({0-3,12-15,20-27}, {4-11,16-19,28-31} and the same + 32,
-  // MI355X_MICROARCH.md section LDS); lane k of group g takes row offset
-  // ro = 2g + (k & 1) and column c = k >> 1, and odd rows read their upper 16
-  // bytes first, so each read of a group covers all 64 banks once.
-  auto expand_segment = [&](const uint32_t* __restrict__ img, uint64_t s) {
+  // ---- expand segment s to odd-only bits, count, store: each lane reads one
+  // block (all 8 planes of 32 periods: 32 contiguous bytes, two
+  // ds_read_b128); wave w takes blocks [kExpandBlocks w, +kExpandBlocks), 64
+  // per step. ds_read_b128 serves a wave in 4 lane groups of 16 ({0-3,12-15,
+  // 20-27}, {4-11,16-19,28-31} and the same + 32, MI355X_MICROARCH.md section
+  // LDS); lane m of group g takes block 16 g + m of the step, and lanes
+  // m >= 8 read their upper 16 bytes first, so each read of a group covers
+  // all 64 banks once. Output words 15 R .. 15 R + 14 of block R: a wave
+  // stores 3,840 contiguous bytes per step.
+  auto expand_segment = [&](const uint32_t* __restrict__ img, uint32_t g_seg) {
+    const uint32_t ri = range_of(g_seg);
+    const WheelRange& rg = wa.r[ri];
+    const uint64_t s = g_seg - rg.seg0;  // the range's segment
+    const uint64_t out_words = 2ull * ((rg.nbits + 63) / 64);  // 32-bit words of the caller's mask
+    uint32_t* __restrict__ out = rg.out;
+    const uint32_t* __restrict__ s_lut = lds.lut[ri];
+    uint32_t my_count = 0;
     uint32_t lane = lane_id;
     asm volatile("" : "+v"(lane));
     const uint32_t l = lane & 31;
     const uint32_t gsub = (l >= 4 && l < 12) || (l >= 16 && l < 20) || l >= 28;
-    const uint32_t k = l < 4 ? l : l < 12 ? l - 4 : l < 20 ? l - 8 : l < 28 ? l - 12 : l - 16;
-    const uint32_t ro = 2 * (2 * (lane >> 5) + gsub) + (k & 1), c = k >> 1;
-    const bool odd = k & 1;
+    const uint32_t m = l < 4 ? l : l < 12 ? l - 4 : l < 20 ? l - 8 : l < 28 ? l - 12 : l - 16;
+    const uint32_t bl = 16 * (2 * (lane >> 5) + gsub) + m;  // block within the step
+    const bool hi_first = m >= 8;
     const uint64_t seg_word0 = s * (uint64_t)kOutWordsPerSeg;
 #pragma unroll 1
-    for (uint32_t t = 0; t < ROWS / (NW * 8); ++t) {
-      const uint32_t row = 8 * ((ROWS / (NW * 8)) * wave + t) + ro;
-      const uint4* rp = reinterpret_cast<const uint4*>(img + row * 64 + 8 * c);
-      const uint4 ra = rp[odd ? 1 : 0], rb = rp[odd ? 0 : 1];
-      const uint4 lo = odd ? rb : ra, hi = odd ? ra : rb;
+    for (uint32_t t = 0; t < kExpandBlocks / 64; ++t) {
+      const uint32_t blk = kExpandBlocks * wave + 64 * t + bl;
+      const uint4* rp = reinterpret_cast<const uint4*>(img + 8 * blk);
+      const uint4 ra = rp[hi_first ? 1 : 0], rb = rp[hi_first ? 0 : 1];
+      const uint4 lo = hi_first ? rb : ra, hi = hi_first ? ra : rb;
       uint32_t W[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};  // composite bits of planes 0..7
       // Transpose every byte column of the 8 x 32 bit matrix in place (rows =
       // planes): afterwards W[j] byte q bit i = plane i, period 8q + j.
@@ -872,10 +871,10 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
           if ((pos & 31) > 17) o[(pos >> 5) + 1] |= e >> (32 - (pos & 31));
         }
       }
-      const uint64_t w0 = seg_word0 + 15ull * (c * ROWS + row);  // caller's 32-bit word index
-      if (s == 0 && c == 0 && row == 0) o[0] |= wa.fix0;
+      const uint64_t w0 = seg_word0 + 15ull * blk;  // caller's 32-bit word index
+      if (s == 0 && blk == 0) o[0] |= rg.fix0;
       const uint64_t bit0 = 32ull * w0;
-      if (bit0 + 480 <= wa.nbits) {  // whole row inside the range (a separate path: no phi copies of o[])
+      if (bit0 + 480 <= rg.nbits) {  // whole block inside the range (a separate path: no phi copies of o[])
         uint32_t cnt = 0;
 #pragma unroll
         for (int w = 0; w < 15; ++w) cnt += __popc(o[w]);
@@ -885,7 +884,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
           for (int w = 0; w < 15; ++w) out[w0 + w] = o[w];
         }
       } else {  // range end (last segment only): mask, count, store what is inside the caller's words
-        const uint32_t rem = bit0 >= wa.nbits ? 0u : (uint32_t)(wa.nbits - bit0);  // < 480 valid bits
+        const uint32_t rem = bit0 >= rg.nbits ? 0u : (uint32_t)(rg.nbits - bit0);  // < 480 valid bits
         uint32_t cnt = 0;
 #pragma unroll
         for (int w = 0; w < 15; ++w) {
@@ -901,11 +900,16 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         }
       }
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) my_count += __shfl_xor(my_count, o);
+    if (lane == 0 && my_count) atomicAdd(&lds.rcnt[ri], (unsigned long long)my_count);
   };
 
   // ---- mark segment s into image img -------------------------------------
-  auto mark_segment = [&](uint32_t* __restrict__ img, uint64_t s) {
-    const uint64_t Vs = wa.V0 + s * kWheelSpan;  // segment base value
+  auto mark_segment = [&](uint32_t* __restrict__ img, uint32_t g_seg) {
+    const WheelRange& rg = wa.r[range_of(g_seg)];
+    const uint64_t s = g_seg - rg.seg0;  // the range's segment
+    const uint64_t Vs = rg.V0 + s * kWheelSpan;  // segment base value
     const uint64_t Vend = Vs + kWheelSpan;
     // Lane-derived values are segment-invariant; left visible, the compiler
     // hoists dozens of them out of the round loop and spills them. Recompute.
@@ -929,8 +933,8 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     }
     const uint32_t rot = (i_mid1 + lane) & 7;  // = table index & 7 of this lane's large primes
     // absolute residue (q + rot) & 7 at step q: its plane and e bit
-    const uint32_t pl_rot = ((wa.pl_pack >> (3 * rot)) | (wa.pl_pack << (24 - 3 * rot))) & 0xFFFFFFu;
-    const uint32_t e_rot = ((wa.e_iota >> rot) | (wa.e_iota << (8 - rot))) & 0xFFu;
+    const uint32_t pl_rot = ((rg.pl_pack >> (3 * rot)) | (rg.pl_pack << (24 - 3 * rot))) & 0xFFFFFFu;
+    const uint32_t e_rot = ((rg.e_iota >> rot) | (rg.e_iota << (8 - rot))) & 0xFFu;
     PlaneSteps ps;
     ps.one = one;
 #pragma unroll
@@ -938,7 +942,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       ps.pb[q] = img0 + 4 * ((pl_rot >> (3 * q)) & 7u);
       ps.ne[q] = 0u - ((e_rot >> q) & 1u);
     }
-    const uint64_t Kb = wa.KB0 + s * (uint64_t)KP;
+    const uint64_t Kb = rg.KB0 + s * (uint64_t)KP;
     // One dynamic queue over both lists, interleaved (list 1 at even, list 2
     // at odd positions while both last). Claims run two units ahead: the LDS
     // atomic for unit j+2 is issued when unit j starts and read when it ends
@@ -1048,18 +1052,23 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
           const uint32_t p = pi & 0xFFFFu;
           const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mid_m[k] >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_mid_m[k]);
-          if ((uint64_t)p * p < Vend) unit_A(img, pi, m, Vs, wa.rho_pack, lane, one);
-        } else {
-          const uint32_t j0 = nA + (k - nA) * 8;
+          if ((uint64_t)p * p < Vend) unit_A(img0, pi, m, Vs, rg.rho_pack, lane, one);
+        } else if (k < nA + nB1) {
+          const uint32_t j0 = nA + (k - nA) * 2;
           const uint32_t pf = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
           if ((uint64_t)pf * pf < Vend)
-            unit_B(img, s_mid_p, s_mid_m, j0, min(8u, n_mid - j0), Vs, Vend, wa.rho_pack, lane, one);
+            unit_B1(img0, s_mid_p, s_mid_m, j0, min(2u, n_b1 - j0), Vs, rg.rho_pack, lane, one);
+        } else {
+          const uint32_t j0 = n_b1 + (k - nA - nB1) * 8;
+          const uint32_t pf = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
+          if ((uint64_t)pf * pf < Vend)
+            unit_B2(img0, s_mid_p, s_mid_m, j0, min(8u, n_mid - j0), Vs, Vend, rg.rho_pack, lane, one);
         }
       } else {
         const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p);
-        if ((uint64_t)p0 * p0 < Vend) unit_L(cur, Vs, Vend, Kb, ps, pl_rot, wa.rho_pack);
+        if ((uint64_t)p0 * p0 < Vend) unit_L(cur, Vs, Vend, Kb, ps, pl_rot, rg.rho_pack);
         const uint32_t p1 = __builtin_amdgcn_readfirstlane(cur1.p);
-        if ((uint64_t)p1 * p1 < Vend) unit_L(cur1, Vs, Vend, Kb, ps, pl_rot, wa.rho_pack);
+        if ((uint64_t)p1 * p1 < Vend) unit_L(cur1, Vs, Vend, Kb, ps, pl_rot, rg.rho_pack);
       }
       cur = nxt;
       cur1 = nxt1;
@@ -1071,7 +1080,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   if (T > 0) init_segment(lds.img, blockIdx.x);
   __syncthreads();
   for (uint32_t t = 0; t < T; ++t) {
-    const uint64_t s = blockIdx.x + (uint64_t)t * grid;
+    const uint32_t s = blockIdx.x + t * grid;
     mark_segment(lds.img, s);
     lds_drain();
     __syncthreads();
@@ -1084,15 +1093,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     __syncthreads();
   }
 
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) my_count += __shfl_xor(my_count, o);
-  if (lane_id == 0) lds.wave_cnt[wave] = my_count;
-  __syncthreads();
-  if (tid == 0) {
-    unsigned long long t = 0;
-    for (uint32_t w = 0; w < NW; ++w) t += lds.wave_cnt[w];
-    if (t) atomicAdd(count_out, t);
-  }
+  if (tid < wa.nranges && lds.rcnt[tid]) atomicAdd(wa.r[tid].count, lds.rcnt[tid]);
 }
 
 #if DSE_WHEEL_MAIN_TU
@@ -1257,14 +1258,14 @@ __device__ __forceinline__ uint64_t bucket_first(uint32_t p, const BucketArgs& b
 // of (period k, plane) in the wheel kernel's image << 5 | k & 31, i.e. the
 // address and bit the wheel kernel ORs, decoded here where the walk has VALU
 // to spare (the fill kernels are bound by their stores), not in the wheel
-// kernel (mark_entry). Word index = row * 64 + 8 * column + plane < 2^15, so
-// an entry is < 2^20.
+// kernel (mark_entry). Word index = 8 * block + plane < 2^15, so an entry is
+// < 2^20.
 __device__ __forceinline__ uint32_t bucket_entry(uint64_t o, const BucketArgs& ba, uint32_t& s) {
   s = ((uint32_t)(o >> kWheelLogKP)) / 30u;  // o < 2^34
   const uint32_t u = (uint32_t)(o - (uint64_t)s * kWheelSpan);
   const uint32_t k = u / 30u, rho = u - 30u * k;
   const uint32_t pl = (uint32_t)(ba.plane_lut >> (3 * (rho >> 1))) & 7u;
-  const uint32_t word = (((k >> 5) & (ROWS - 1)) << 6) | ((k >> LOG_LS) << 3) | pl;
+  const uint32_t word = ((k >> 5) << 3) | pl;  // block k >> 5, plane pl
   return (word << 5) | (k & 31u);
 }
 
@@ -1741,14 +1742,18 @@ hipError_t free_scratch(Scratch* s) {
 namespace {
 
 
-// Launch geometry shared by the wheel kernel and the bucket walks.
-[[maybe_unused]] WheelArgs make_wheel_args(uint64_t g_start, uint64_t nbits, uint64_t* plane_lut) {
-  WheelArgs wa{};
-  const uint64_t v_start = 3 + 2 * g_start;
-  wa.V0 = v_start - 1;
-  wa.nbits = nbits;
-  wa.KB0 = wa.V0 / 30;
-  const uint32_t v0m = (uint32_t)(wa.V0 % 30);
+// One range's geometry (shared by the wheel kernel and the bucket walks):
+// the planes of V0 mod 30, the small-prime fixes, the init offsets.
+// *plane_lut: plane of relative residue rho in bits [3 (rho >> 1), +3).
+[[maybe_unused]] WheelRange make_wheel_range(const RangeSpec& rs, uint64_t* plane_lut) {
+  WheelRange w{};
+  const uint64_t v_start = 3 + 2 * rs.g_start;
+  w.V0 = v_start - 1;
+  w.nbits = rs.nbits;
+  w.KB0 = w.V0 / 30;
+  w.out = rs.out;
+  w.count = rs.count;
+  const uint32_t v0m = (uint32_t)(w.V0 % 30);
   uint32_t n = 0;
   *plane_lut = 0;
   for (uint32_t rho = 1; rho < 30; rho += 2) {
@@ -1756,31 +1761,46 @@ namespace {
     if (r % 3 == 0 || r % 5 == 0) continue;
     uint32_t iota = 0;
     while (kR30[iota] != r) ++iota;
-    wa.rho_pack |= (uint64_t)rho << (5 * n);
-    wa.pl_pack |= n << (3 * iota);
-    if (v0m + rho >= 30) wa.e_iota |= 1u << iota;
+    w.rho_pack |= (uint64_t)rho << (5 * n);
+    w.pl_pack |= n << (3 * iota);
+    if (v0m + rho >= 30) w.e_iota |= 1u << iota;
     *plane_lut |= (uint64_t)n << (3 * (rho >> 1));
     ++n;
   }
   // primes 3..61 inside the range: the wheel drops 3 and 5, the patterns mark 7..61 themselves
   constexpr uint32_t small[] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61};
   for (uint32_t v : small)
-    if (v >= v_start && (v - v_start) / 2 < nbits) wa.fix0 |= 1u << ((v - v_start) / 2);
-  // odd primes up to 61, TA, TB and kWheelMaxPrime (sieved once)
+    if (v >= v_start && (v - v_start) / 2 < rs.nbits) w.fix0 |= 1u << ((v - v_start) / 2);
+  for (int g = 0; g < kNG; ++g) w.v0g[g] = (uint16_t)(w.V0 % gmod(g));
+  return w;
+}
+
+// A launch over the ranges rs[0..n) (1 <= n <= kMaxRanges, each < 2^31
+// segments in all), their segments in order; thresholds: odd primes up to
+// 61, TA, TB1, TB and kWheelMaxPrime (sieved once).
+[[maybe_unused]] WheelArgs make_wheel_args(const RangeSpec* rs, uint32_t n, uint64_t* plane_lut) {
   static const auto counts = [] {
-    std::array<uint32_t, 4> c{};
-    const uint32_t lim[4] = {kQMax, TA, TB, (uint32_t)kWheelMaxPrime};
+    std::array<uint32_t, 5> c{};
+    const uint32_t lim[5] = {kQMax, TA, TB1, TB, (uint32_t)kWheelMaxPrime};
     std::vector<uint8_t> comp(kWheelMaxPrime / 2 + 1, 0);  // comp[i]: 2i + 1 composite
     for (uint64_t i = 1; (2 * i + 1) * (2 * i + 1) <= kWheelMaxPrime; ++i)
       if (!comp[i])
         for (uint64_t j = ((2 * i + 1) * (2 * i + 1)) / 2; j <= kWheelMaxPrime / 2; j += 2 * i + 1) comp[j] = 1;
     for (uint64_t i = 1; 2 * i + 1 <= kWheelMaxPrime; ++i)
       if (!comp[i])
-        for (int t = 0; t < 4; ++t) c[t] += 2 * i + 1 <= lim[t];
+        for (int t = 0; t < 5; ++t) c[t] += 2 * i + 1 <= lim[t];
     return c;
   }();
-  for (int t = 0; t < 4; ++t) wa.nthr[t] = counts[t];
-  for (int g = 0; g < kNG; ++g) wa.v0g[g] = (uint16_t)(wa.V0 % gmod(g));
+  WheelArgs wa{};
+  for (int t = 0; t < 5; ++t) wa.nthr[t] = counts[t];
+  uint64_t seg = 0, lut = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    wa.r[i] = make_wheel_range(rs[i], i ? &lut : plane_lut);
+    wa.r[i].seg0 = (uint32_t)seg;
+    seg += (rs[i].nbits + kWheelOutBits - 1) / kWheelOutBits;
+  }
+  wa.nranges = n;
+  wa.nseg = (uint32_t)seg;
   return wa;
 }
 
@@ -1863,20 +1883,31 @@ hipError_t release_scratch(Scratch* sc, hipStream_t stream) {
 
 #endif  // DSE_WHEEL_MAIN_TU
 
-hipError_t launch_wheel(const void* table, const WheelArgs& wa, uint32_t* out, unsigned long long* count,
-                        int num_cus, hipStream_t stream) {
-  const uint64_t nseg = (wa.nbits + kWheelOutBits - 1) / kWheelOutBits;
-  const uint64_t grid = nseg < (uint64_t)num_cus ? nseg : (uint64_t)num_cus;
+hipError_t launch_wheel(const void* table, const WheelArgs& wa, int num_cus, hipStream_t stream) {
+  if (wa.nseg == 0) return hipSuccess;
+  const uint32_t grid = std::min<uint32_t>(wa.nseg, (uint32_t)num_cus);
 #if DSE_WHEEL_MAIN_TU
   // ranges without bucketed primes: the no-bucket instantiation, compiled in
   // dse_wheel_plain.hip with the default machine scheduler (its loop spills
   // fewer SGPRs there; the bucket instantiation is faster with iterative-ILP)
-  if (!wa.bk_start) return launch_wheel_plain(table, &wa, out, count, num_cus, stream);
-  hipLaunchKernelGGL(wheel_segments_kernel<true>, dim3((uint32_t)grid), dim3(NT), 0, stream, table, wa, out, count);
+  if (!wa.bk_start) return launch_wheel_plain(table, &wa, num_cus, stream);
+  hipLaunchKernelGGL(wheel_segments_kernel<true>, dim3(grid), dim3(NT), 0, stream, table, wa);
 #else
-  hipLaunchKernelGGL(wheel_segments_kernel<false>, dim3((uint32_t)grid), dim3(NT), 0, stream, table, wa, out, count);
+  hipLaunchKernelGGL(wheel_segments_kernel<false>, dim3(grid), dim3(NT), 0, stream, table, wa);
 #endif
   return hipGetLastError();
+}
+
+// Launches over rs[0..n), kMaxRanges ranges at a time.
+[[maybe_unused]] hipError_t launch_wheel_batches(const void* table, const RangeSpec* rs, size_t n, int num_cus,
+                                                 hipStream_t stream) {
+  for (size_t i = 0; i < n; i += kMaxRanges) {
+    uint64_t plane_lut;
+    const hipError_t e = launch_wheel(
+        table, make_wheel_args(rs + i, (uint32_t)std::min<size_t>(kMaxRanges, n - i), &plane_lut), num_cus, stream);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace
@@ -1885,19 +1916,16 @@ hipError_t launch_wheel(const void* table, const WheelArgs& wa, uint32_t* out, u
 // The full-geometry wheel kernel for ranges without bucketed primes (N up to
 // 1.1e12), on its own translation unit for its compile flags (Makefile).
 // wa: the caller's WheelArgs (the same definition, this source).
-hipError_t launch_wheel_plain(const void* table, const void* wa, uint32_t* out, unsigned long long* count,
-                              int num_cus, hipStream_t stream) {
-  return launch_wheel(table, *static_cast<const WheelArgs*>(wa), out, count, num_cus, stream);
+hipError_t launch_wheel_plain(const void* table, const void* wa, int num_cus, hipStream_t stream) {
+  return launch_wheel(table, *static_cast<const WheelArgs*>(wa), num_cus, stream);
 }
 #elif DSE_WHEEL_HALF_TU
 // The half-size geometry (this translation unit: 2^16 periods per segment):
-// the tail of a range whose last round of full segments would leave most
-// CUs idle (launch_sieve_range). Primes <= kWheelMaxPrime only.
-hipError_t launch_wheel_range_half(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
-                                   unsigned long long* count, int num_cus, hipStream_t stream) {
-  if (nbits == 0) return hipSuccess;
-  uint64_t plane_lut;
-  return launch_wheel(table, make_wheel_args(g_start, nbits, &plane_lut), out, count, num_cus, stream);
+// the tail of a launch whose last round of full segments would leave most
+// CUs idle (launch_sieve_ranges). Primes <= kWheelMaxPrime only.
+hipError_t launch_wheel_ranges_half(const void* table, const RangeSpec* rs, size_t n, int num_cus,
+                                    hipStream_t stream) {
+  return launch_wheel_batches(table, rs, n, num_cus, stream);
 }
 #else
 // Time of a half-size segment (dse_wheel_half.hip) relative to a full one,
@@ -1905,34 +1933,56 @@ hipError_t launch_wheel_range_half(const void* table, uint64_t g_start, uint64_t
 // (profiles/r03/geometry_ab.txt).
 constexpr double kHalfSegCost = DSE_HALF_SEG_COST, kLaunchCost = DSE_LAUNCH_COST;
 
-hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
-                              unsigned long long* count, int num_cus, hipStream_t stream, Scratch* scratch,
-                              const SieveOpts* opts) {
-  if (nbits == 0) return hipSuccess;
+namespace {
+
+// The ranges without bucketed primes, pooled: one persistent launch (per
+// kMaxRanges ranges) over all their segments. Segments go to the num_cus
+// workgroups in rounds; a last, partial round of full segments leaves CUs
+// idle for a whole segment time, so the segments past the last full round
+// go to the half-size geometry instead when that finishes sooner: (their
+// half segments / num_cus rounds) x kHalfSegCost plus the second launch.
+hipError_t launch_pooled(const void* table, const RangeSpec* rs, size_t n, int num_cus, hipStream_t stream,
+                         const SieveOpts* opts) {
+  if (n == 0) return hipSuccess;
+  const uint32_t geo = opts ? opts->wheel_geometry : 0;  // 0 auto, 1 full only, 2 half only
+  constexpr uint64_t kHalfBits = kWheelOutBits / 2;
+  const uint64_t G = (uint64_t)num_cus;
+  uint64_t S = 0;
+  for (size_t i = 0; i < n; ++i) S += (rs[i].nbits + kWheelOutBits - 1) / kWheelOutBits;
+  uint64_t F = geo == 2 ? 0 : geo == 1 ? S : (S / G) * G;  // segments of the full geometry
+  // split the list after its first F full segments
+  std::vector<RangeSpec> full, half;
+  uint64_t left = F;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t ns = (rs[i].nbits + kWheelOutBits - 1) / kWheelOutBits;
+    const uint64_t take = std::min(ns, left);
+    left -= take;
+    const uint64_t fb = std::min(rs[i].nbits, take * kWheelOutBits);
+    if (fb) full.push_back({rs[i].g_start, fb, rs[i].out, rs[i].count});
+    if (fb < rs[i].nbits)
+      half.push_back({rs[i].g_start + fb, rs[i].nbits - fb, rs[i].out ? rs[i].out + fb / 32 : nullptr,
+                      rs[i].count});
+  }
+  if (geo == 0 && !half.empty()) {
+    uint64_t nhalf = 0;
+    for (const auto& h : half) nhalf += (h.nbits + kHalfBits - 1) / kHalfBits;
+    if (kHalfSegCost * (double)((nhalf + G - 1) / G) + (F ? kLaunchCost : 0.0) >= 1.0) {
+      half.clear();  // the whole list in the full geometry
+      full.assign(rs, rs + n);
+    }
+  }
+  hipError_t e = launch_wheel_batches(table, full.data(), full.size(), num_cus, stream);
+  if (e != hipSuccess) return e;
+  return half.empty() ? hipSuccess : launch_wheel_ranges_half(table, half.data(), half.size(), num_cus, stream);
+}
+
+// A range whose primes reach above kWheelMaxPrime: bucketed passes.
+hipError_t launch_bucketed(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
+                           unsigned long long* count, int num_cus, hipStream_t stream, Scratch* scratch,
+                           const SieveOpts* opts) {
   const uint64_t vmax = 3 + 2 * (g_start + nbits - 1);
   const uint64_t root = isqrt64(vmax);
   uint64_t plane_lut;
-  if (root <= kWheelMaxPrime) {
-    // Segments go to the num_cus persistent workgroups in rounds; a last,
-    // partial round of full segments leaves CUs idle for a whole segment
-    // time. Its range goes to the half-size geometry instead when that
-    // finishes sooner: (its segments / num_cus rounds) x kHalfSegCost plus
-    // the second launch.
-    const uint32_t geo = opts ? opts->wheel_geometry : 0;  // 0 auto, 1 full only, 2 half only
-    const uint64_t G = (uint64_t)num_cus, nseg = (nbits + kWheelOutBits - 1) / kWheelOutBits;
-    uint64_t F = geo == 2 ? 0 : geo == 1 ? nseg : (nseg / G) * G;  // segments of the full geometry
-    if (geo == 0 && F < nseg) {
-      const uint64_t nhalf = (nbits - F * kWheelOutBits + kWheelOutBits / 2 - 1) / (kWheelOutBits / 2);
-      if (kHalfSegCost * (double)((nhalf + G - 1) / G) + (F ? kLaunchCost : 0.0) >= 1.0) F = nseg;
-    }
-    if (F >= nseg) return launch_wheel(table, make_wheel_args(g_start, nbits, &plane_lut), out, count, num_cus, stream);
-    hipError_t e;
-    if (F && (e = launch_wheel(table, make_wheel_args(g_start, F * kWheelOutBits, &plane_lut), out, count, num_cus,
-                               stream)) != hipSuccess)
-      return e;
-    return launch_wheel_range_half(table, g_start + F * kWheelOutBits, nbits - F * kWheelOutBits,
-                                   out ? out + F * (kWheelOutBits / 32) : nullptr, count, num_cus, stream);
-  }
   if (!scratch) return hipErrorInvalidValue;
   // primes above kWheelMaxPrime: passes of <= kBucketMaxSegs segments, each
   // with its own bucket build, then the wheel kernel over the pass
@@ -1945,17 +1995,19 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
   const double a0 = (double)kWheelMaxPrime, b0 = std::min((double)split, (double)root);  // band 0: (a0, b0]
   for (uint64_t s0 = 0; s0 < total_seg;) {
     uint64_t ns = std::min<uint64_t>(max_segs, total_seg - s0);
-    WheelArgs wa = make_wheel_args(g_start + s0 * kWheelOutBits, kWheelOutBits, &plane_lut);  // (wa.nthr)
-    const uint32_t k0_full = bucket_k0(wa.nthr[3], a0, b0);
+    RangeSpec piece{g_start + s0 * kWheelOutBits, kWheelOutBits, nullptr, count};
+    WheelArgs wa = make_wheel_args(&piece, 1, &plane_lut);  // (wa.nthr)
+    const uint32_t k0_full = bucket_k0(wa.nthr[4], a0, b0);
     while (ns > 1 && (bucket_cap(ns * kWheelSpan, (double)split, (double)root) > kBucketMaxEntries ||
                       4ull * ns * kBucketGrid * k0_full > kBucketMaxRegionBytes))
       ns /= 2;
     const uint64_t g0 = g_start + s0 * kWheelOutBits;
     const uint64_t nb = std::min<uint64_t>(nbits - s0 * kWheelOutBits, ns * kWheelOutBits);
     const uint64_t vmax_p = 3 + 2 * (g0 + nb - 1);
-    wa = make_wheel_args(g0, nb, &plane_lut);
+    piece = {g0, nb, out ? out + s0 * (kWheelOutBits / 32) : nullptr, count};
+    wa = make_wheel_args(&piece, 1, &plane_lut);
     BucketArgs ba{};
-    ba.V0 = wa.V0;
+    ba.V0 = wa.r[0].V0;
     ba.span = ns * kWheelSpan;
     ba.plane_lut = plane_lut;
     ba.nseg = (uint32_t)ns;
@@ -2031,13 +2083,41 @@ hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbit
     wa.bk_nspill = bz.nspill;
     wa.bk_spill_cap = spill_cap;
     wa.bk_k0 = k0;
-    if ((e = launch_wheel(table, wa, out ? out + s0 * (kWheelOutBits / 32) : nullptr, count, num_cus, stream)) !=
-        hipSuccess)
-      return fail_pass(e);
+    if ((e = launch_wheel(table, wa, num_cus, stream)) != hipSuccess) return fail_pass(e);
     if ((e = release_scratch(scratch, stream)) != hipSuccess) return e;
     s0 += ns;
   }
   return hipSuccess;
+}
+
+}  // namespace
+
+hipError_t launch_sieve_ranges(const void* table, const RangeSpec* rs, size_t n, int num_cus, hipStream_t stream,
+                               Scratch* scratch, const SieveOpts* opts) {
+  // ranges of up to 2^30 segments (the launch's 32-bit segment indices)
+  constexpr uint64_t kMaxBits = (1ull << 30) * kWheelOutBits;
+  std::vector<RangeSpec> pooled;
+  for (size_t i = 0; i < n; ++i) {
+    for (uint64_t b = 0; b < rs[i].nbits; b += kMaxBits) {
+      const RangeSpec piece{rs[i].g_start + b, std::min(kMaxBits, rs[i].nbits - b),
+                            rs[i].out ? rs[i].out + b / 32 : nullptr, rs[i].count};
+      if (isqrt64(3 + 2 * (piece.g_start + piece.nbits - 1)) <= kWheelMaxPrime) {
+        pooled.push_back(piece);
+      } else {
+        const hipError_t e = launch_bucketed(table, piece.g_start, piece.nbits, piece.out, piece.count, num_cus,
+                                             stream, scratch, opts);
+        if (e != hipSuccess) return e;
+      }
+    }
+  }
+  return launch_pooled(table, pooled.data(), pooled.size(), num_cus, stream, opts);
+}
+
+hipError_t launch_sieve_range(const void* table, uint64_t g_start, uint64_t nbits, uint32_t* out,
+                              unsigned long long* count, int num_cus, hipStream_t stream, Scratch* scratch,
+                              const SieveOpts* opts) {
+  const RangeSpec rs{g_start, nbits, out, count};
+  return launch_sieve_ranges(table, &rs, 1, num_cus, stream, scratch, opts);
 }
 #endif  // DSE_WHEEL_HALF_TU
 

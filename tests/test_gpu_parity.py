@@ -575,3 +575,28 @@ def test_segment_geometries_vs_oracle(oracle, geometry):
             m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
             m, cnt = c.sieve_odd_range(g0, nb)
             assert cnt == c_ref and np.array_equal(m, m_ref), (geometry, g0, nb)
+
+
+@pytest.mark.parametrize("geometry", [0, 1, 2])
+def test_pooled_chunks_vs_oracle(oracle, geometry):
+    """Several chunks of one device in one launch (launch_sieve_ranges pools a
+    device's chunks and the dropped tail; more than 9 ranges go in batches):
+    every chunk mask and count of random (N, P), P up to 20, against the
+    oracle, with the segments past the last full round in the half-size
+    geometry (0, when it pays), all full (1) or all half (2)."""
+    from mail_sieve_e import sieve as S
+    rng = np.random.default_rng(0xB10C + geometry)
+    cases = [(10**9, 8), (2 * 10**8 + 7, 11), (10**7 + 1, 20)]
+    cases += [(int(rng.integers(10**6, 3 * 10**8)), int(rng.integers(1, 21))) for _ in range(6)]
+    with S.Context(num_gpus=1) as c:
+        c.debug_set_option("wheel_geometry", geometry)
+        for N, P in cases:
+            cs = (N - 1) // 2 // P
+            tail_g, tail_n = oracle.tail_range(N, P)
+            counts, pi_ref, pi_full = c.sieve_all(N, P)
+            for k in range(P):
+                m_ref, c_ref = oracle.fast_sieve_range(k * cs, cs)
+                assert int(counts[k]) == c_ref, (geometry, N, P, k)
+                assert np.array_equal(c.copy_chunk_mask(N, P, k + 1), m_ref), (geometry, N, P, k)
+            t_ref = oracle.fast_sieve_range(tail_g, tail_n, want_mask=False)[1] if tail_n else 0
+            assert pi_full - pi_ref == t_ref, (geometry, N, P)
