@@ -67,7 +67,7 @@ constexpr uint32_t NT = 1024;
 constexpr uint32_t NW = NT / 64;            // waves; every wave marks, expands and inits
 static_assert(BLOCKS % (64 * NW) == 0, "expansion blocks");
 #ifndef DSE_TA
-#define DSE_TA 256
+#define DSE_TA 96
 #endif
 #ifndef DSE_WHEEL_HALF_TU
 #define DSE_WHEEL_HALF_TU 0  // 1: compiled by dse_wheel_half.hip with 2^16 periods per segment
@@ -84,11 +84,11 @@ static_assert(BLOCKS % (64 * NW) == 0, "expansion blocks");
 #endif
 constexpr uint32_t TA = DSE_TA;             // A/B1 threshold
 #ifndef DSE_TB1
-#define DSE_TB1 1024
+#define DSE_TB1 384
 #endif
 constexpr uint32_t TB1 = DSE_TB1;           // B1/B2 threshold
 #ifndef DSE_TB
-#define DSE_TB 4096
+#define DSE_TB 1536
 #endif
 constexpr uint32_t TB = DSE_TB;             // B2/L threshold
 static_assert(TA <= 256 && TA < TB1 && TB1 <= TB && TB <= KP / 8, "unit thresholds");
@@ -528,7 +528,24 @@ __device__ __forceinline__ void load_L(LargeOps& o, const uint32_t* __restrict__
 // block conflicts like a mark).
 template <bool PRED>
 __device__ __forceinline__ void mark_plane(uint32_t pb4, uint32_t kk, uint32_t one) {
-  if (PRED && kk >= KP) return;
+  if (PRED) {
+    // exec &= (kk < KP) for the one mark, restored after it: 1 VALU + 2 SALU
+    // where the compiler's if takes a compare, saveexec, branch and restore
+    // (1e12: -2.2%, profiles/r04/ab_threshold_grid2_1e12.txt)
+    uint64_t sv;
+    uint32_t a, b;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %3, %4\n\t"
+        "v_and_or_b32 %1, %4, %5, %6\n\t"
+        "v_lshlrev_b32 %2, %4, %7\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(sv), "=&v"(a), "=&v"(b)
+        : "s"(KP), "v"(kk), "s"(kBlockMask), "v"(pb4), "v"(one)
+        : "memory", "vcc");
+    return;
+  }
   mark_k(pb4, kk, one);
 }
 
@@ -612,6 +629,17 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
   if (Kb < (1ull << 32)) {
     const uint32_t q = (uint32_t)((float)(uint32_t)Kb * invp);
     uint32_t x = (uint32_t)Kb - __umul24(q, p);  // in (-p, 2p) as a signed value; p < 2^24
+    x = min(x, x + p);
+    kbm = min(x, x - p);
+  } else if (Kb < (1ull << 38)) {
+    // values below 8.2e12: the float quotient of Kb is within 17 of the true
+    // one (relative error < 2^-22, Kb / p < 2^26), so Kb - q p is exact in 32
+    // bits (|.| < 18 p < 2^25); one more float quotient of that rest leaves
+    // it in (-p, p). 12 VALU where the 64-bit Barrett reduction takes ~24.
+    const uint32_t q = (uint32_t)((float)Kb * invp);
+    const int32_t r = (int32_t)((uint32_t)Kb - q * p);
+    const int32_t q2 = (int32_t)((float)r * invp);
+    uint32_t x = (uint32_t)(r - __mul24(q2, (int32_t)p));
     x = min(x, x + p);
     kbm = min(x, x - p);
   } else {

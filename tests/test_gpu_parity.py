@@ -347,11 +347,13 @@ def test_table_from_broadcast_primes(ctx, limit):
     assert outs[0][1] == outs[1][1] > 0 and torch.equal(outs[0][0], outs[1][0])
 
 
-def test_kb_float_quotient_boundary(ctx, oracle):
-    """The L units take Kb mod p from a float quotient while Kb = floor(V/30)
-    < 2^32 and from a 64-bit Barrett reduction above: a range straddling
-    V = 30 * 2^32 (segments on both sides) against the oracle."""
-    v = 30 * 2**32
+@pytest.mark.parametrize("log_kb", [32, 38])
+def test_kb_float_quotient_boundary(ctx, oracle, log_kb):
+    """The L units take Kb mod p from one float quotient while Kb =
+    floor(V/30) < 2^32, from two up to 2^38 and from a 64-bit Barrett
+    reduction above: ranges straddling V = 30 * 2^32 and 30 * 2^38
+    (segments on both sides) against the oracle."""
+    v = 30 * 2**log_kb
     g0 = (v - 3) // 2 - 3 * 1966080 + 12345
     nb = 6 * 1966080 + 777
     m, c = ctx.sieve_odd_range(g0, nb)
