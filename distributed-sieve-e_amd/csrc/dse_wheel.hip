@@ -124,7 +124,8 @@ constexpr uint32_t gmod(int g) { return kGQ[g][0] * kGQ[g][1] * kGQ[g][2]; }
 constexpr uint32_t kInitWords = IMG_WORDS / NT;  // words one lane inits per segment (one plane of a block run)
 constexpr uint32_t kInitRun = 32 * kInitWords;    // their periods
 constexpr uint32_t kExpandBlocks = BLOCKS / NW;   // blocks one wave expands (and inits) per segment
-constexpr uint32_t kInitBlocks = kInitRun / 128 + 1;  // ds_read_b128 per lane and group
+// ds_read_b128 per lane and group (+1: a staggered run's one word more, read as one more pass)
+constexpr uint32_t kInitBlocks = kInitRun / 128 + 2;
 // dwords per group string and copy: the reads reach dword d0 + 4 kInitBlocks - 1, d0 < M_G/32 + 1
 constexpr uint32_t gdw(int g) { return ((gmod(g) + 32 * (4 * kInitBlocks + 1) + 127) / 128) * 4; }
 constexpr uint32_t gbase(int g) { return g == 0 ? 0u : gbase(g - 1) + gdw(g - 1); }
@@ -393,15 +394,37 @@ __device__ __forceinline__ void a_classes(uint32_t pb4, uint32_t k, uint32_t p, 
   }
 }
 
+// Vs mod p of the staged mid primes, carried from segment to segment: a
+// workgroup's next segment starts G W integers later (G workgroups), so the
+// unit that uses x[i] for this segment leaves (x[i] + inc[i]) mod p there,
+// inc[i] = G W mod p. `have`: x holds this segment's residues (the
+// workgroup's previous segment was of the same range and every mid unit ran
+// in it); otherwise a 64-bit Barrett reduction (the workgroup's first
+// segment, a range change, segments below TB^2).
+struct MidRes {
+  uint32_t* x;
+  const uint32_t* inc;
+  bool have;
+};
+__device__ __forceinline__ uint32_t mid_residue(const MidRes& mr, uint32_t i, uint32_t p, uint64_t m, uint64_t Vs,
+                                                bool writer) {
+  const uint32_t xs = mr.have ? mr.x[i] : mod_barrett(Vs, p, m);
+  if (writer) {
+    const uint32_t t = xs + mr.inc[i];
+    mr.x[i] = min(t, t - p);
+  }
+  return xs;
+}
+
 // A: one mid prime (61 < p <= TA) per wave; lane (plane L & 7, c = L >> 3).
 // Lanes 0-31 have c = 0..3: a plane's four lanes mark 32p periods apart at
 // every step (same class r, same t), i.e. in blocks c p (mod 4) apart -- four
 // distinct banks for odd p.
-__device__ __forceinline__ void unit_A(uint32_t img0, uint32_t pi, uint64_t m, uint64_t Vs, uint64_t rho_pack,
-                                       uint32_t lane, uint32_t one) {
+__device__ __forceinline__ void unit_A(uint32_t img0, uint32_t pi, uint64_t m, const MidRes& mr, uint32_t idx,
+                                       uint64_t Vs, uint64_t rho_pack, uint32_t lane, uint32_t one) {
   const uint32_t p = pi & 0xFFFFu, inv30 = pi >> 16;  // wave-uniform
   const uint64_t p2 = (uint64_t)p * p;
-  const uint32_t Xs = mod_barrett(Vs, p, m);            // scalar unit
+  const uint32_t Xs = __builtin_amdgcn_readfirstlane(mid_residue(mr, idx, p, m, Vs, lane == 0));
   const float invp = fast_rcp((float)p);
   const uint32_t pl = lane & 7, c = lane >> 3;
   const uint32_t rho = (uint32_t)(rho_pack >> (5 * pl)) & 31u;
@@ -435,8 +458,8 @@ __device__ __forceinline__ void unit_A(uint32_t img0, uint32_t pi, uint64_t m, u
 // lane fills are unrolled without a test; the last one, partly filled, is
 // marked with a per-lane count.
 __device__ __forceinline__ void unit_B1(uint32_t img0, const uint32_t* __restrict__ s_mid_p,
-                                        const uint64_t* __restrict__ s_mid_m, uint32_t j0, uint32_t nj, uint64_t Vs,
-                                        uint64_t rho_pack, uint32_t lane, uint32_t one) {
+                                        const uint64_t* __restrict__ s_mid_m, const MidRes& mr, uint32_t j0,
+                                        uint32_t nj, uint64_t Vs, uint64_t rho_pack, uint32_t lane, uint32_t one) {
   const uint32_t h = lane >> 5, pl = lane & 7, j = (lane >> 3) & 3;
   if (h >= nj) return;  // the unit's second half-wave when the list ends
   const uint32_t pi = s_mid_p[j0 + h];
@@ -444,7 +467,7 @@ __device__ __forceinline__ void unit_B1(uint32_t img0, const uint32_t* __restric
   const uint64_t m = s_mid_m[j0 + h];
   const float invp = fast_rcp((float)p);
   const uint32_t rho = (uint32_t)(rho_pack >> (5 * pl)) & 31u;
-  const uint32_t kp = plane_first(mod_barrett(Vs, p, m), rho, p, inv30, invp);
+  const uint32_t kp = plane_first(mid_residue(mr, j0 + h, p, m, Vs, (lane & 31) == 0), rho, p, inv30, invp);
   const uint32_t pb4 = img0 + 4 * pl;
   uint32_t k = kp + 32 * j * p;                          // hit n = 32j
   const uint64_t p2 = (uint64_t)p * p;
@@ -478,8 +501,9 @@ __device__ __forceinline__ void unit_B1(uint32_t img0, const uint32_t* __restric
 // lane, then a short per-lane tail. A plane's lanes hold different primes,
 // so their banks collide at random (the L pattern).
 __device__ __forceinline__ void unit_B2(uint32_t img0, const uint32_t* __restrict__ s_mid_p,
-                                        const uint64_t* __restrict__ s_mid_m, uint32_t j0, uint32_t nj, uint64_t Vs,
-                                        uint64_t Vend, uint64_t rho_pack, uint32_t lane, uint32_t one) {
+                                        const uint64_t* __restrict__ s_mid_m, const MidRes& mr, uint32_t j0,
+                                        uint32_t nj, uint64_t Vs, uint64_t Vend, uint64_t rho_pack, uint32_t lane,
+                                        uint32_t one) {
   const uint32_t pl = lane & 7, jp = lane >> 3;
   const bool valid = jp < nj;
   const uint32_t pi = s_mid_p[valid ? j0 + jp : j0];
@@ -487,7 +511,7 @@ __device__ __forceinline__ void unit_B2(uint32_t img0, const uint32_t* __restric
   const uint64_t m = s_mid_m[valid ? j0 + jp : j0];
   const float invp = fast_rcp((float)p);
   const uint32_t rho = (uint32_t)(rho_pack >> (5 * pl)) & 31u;
-  uint32_t k = plane_first(mod_barrett(Vs, p, m), rho, p, inv30, invp);
+  uint32_t k = plane_first(mid_residue(mr, valid ? j0 + jp : j0, p, m, Vs, valid && pl == 0), rho, p, inv30, invp);
   const uint64_t p2 = (uint64_t)p * p;
   const bool slow = p2 > Vs;
   if (slow) k = p2 >= Vend ? KP : first_at_or_after(k, kmin_for((uint32_t)(p2 - Vs), rho), p, invp);
@@ -697,6 +721,9 @@ struct WheelLds {
   uint32_t img[IMG_WORDS];         // the segment image, at LDS address 0
   uint64_t mid_m[kMidCap];         // Barrett factors of the staged mid primes
   uint32_t mid_p[kMidCap];         // p | (30^{-1} mod p) << 16
+  uint32_t mid_x[kMidCap];         // Vs mod p of this workgroup's segment (MidRes)
+  uint32_t mid_inc[kMidCap];       // G W mod p
+  uint32_t x_seg;                  // the launch segment mid_x holds (~0: none)
   uint32_t lut[kMaxRanges][256];   // per range: period byte -> 15 odd slots
   uint4 itab[kGDW];                // init tables U_G, 4 copies shifted by 0..3 dwords (kGDW / 4 blocks each)
   uint32_t thr[5];
@@ -739,6 +766,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     s_thr[2] = min(s_thr[2], s_thr[3]);
     s_thr[4] = max(s_thr[3], min(wa.nthr[4], np));
     lds.ctr = 0;
+    lds.x_seg = ~0u;
   }
   if (tid < kMaxRanges) lds.rcnt[tid] = 0;
   for (uint32_t x = tid; x < 256 * wa.nranges; x += NT) {
@@ -761,6 +789,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     const uint32_t q = P[i_mid0 + i];
     s_mid_p[i] = q | ((uint32_t)inv30_of(q) << 16);  // p < 2^14, 30^{-1} mod p < p
     s_mid_m[i] = M[i_mid0 + i];
+    lds.mid_inc[i] = (uint32_t)(((uint64_t)gridDim.x * kWheelSpan) % q);
   }
   // Work units: list 1 = nA single mid primes (A), nB1 units of two primes
   // (B1), nB2 units of 8 primes (B2); list 2 = nL large units (two sets of 64
@@ -789,8 +818,9 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
 
   // ---- init: small-prime patterns (7..61) of segment s into the image. Lane
   // (plane L & 7, run q = 8 w + (L >> 3)) of wave w writes its plane's words
-  // of the kInitWords consecutive blocks [kInitWords q, +kInitWords): the
-  // blocks this wave expands, so it may init them right after expanding.
+  // of a run of about kInitWords consecutive blocks inside the wave's
+  // [kExpandBlocks w, +kExpandBlocks): the blocks this wave expands, so it
+  // may init them right after expanding.
   auto init_segment = [&](uint32_t* __restrict__ img, uint32_t g_seg) {
     const WheelRange& rg = wa.r[range_of(g_seg)];
     const uint64_t s = g_seg - rg.seg0;  // the range's segment
@@ -799,7 +829,14 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     const uint32_t pl = lane & 7, q = 8 * wave + (lane >> 3);
     const uint32_t rho = (uint32_t)(rg.rho_pack >> (5 * pl)) & 31u;
     constexpr uint32_t R = kInitWords;  // words per lane
-    const uint32_t b0 = R * q;          // first block of the run
+    static_assert(R % 4 == 0, "staggered init runs");
+    // a half-wave's four lanes of one plane (j = 0..3) cover a region of 4R
+    // blocks with runs of R + 1, R + 1, R + 1 and R - 3 blocks starting at
+    // (R + 1) j: at step r they write blocks j + r (mod 4) -- distinct banks
+    // (runs of R from multiples of R put all four on one bank: 4-way, 1%
+    // of the kernel, profiles/r04/ab_init_stagger_1e11.txt)
+    const uint32_t j = q & 3;
+    const uint32_t b0 = 4 * R * (q >> 2) + (R + 1) * j;
     const uint32_t k0 = 32 * b0;        // its first period
     constexpr uint32_t H = 16;          // words per pass (bounds the registers: 16 acc + 20 read)
     static_assert(R % H == 0 && H % 4 == 0, "init passes");
@@ -839,7 +876,20 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         asm volatile("" ::: "memory");  // keep the next group's reads after these (register pressure)
       }
 #pragma unroll
-      for (uint32_t r = 0; r < H; ++r) wp[8 * (h + r)] = acc[r];
+      for (uint32_t r = 0; r < H; ++r) {
+        if (h + r >= R - 3 && j == 3) continue;  // the short run
+        wp[8 * (h + r)] = acc[r];
+      }
+    }
+    if (j != 3) {  // word R of the long runs
+      uint32_t acc = 0;
+#pragma unroll
+      for (int g = 0; g < kNG; ++g) {
+        const uint4* bp = lds.itab + boff[g] + R / 4;
+        const uint4 v = bp[0];
+        acc |= __builtin_amdgcn_alignbit(v.y, v.x, bsh[g]);
+      }
+      wp[8 * R] = acc;
     }
   };
 
@@ -971,6 +1021,10 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       ps.ne[q] = 0u - ((e_rot >> q) & 1u);
     }
     const uint64_t Kb = rg.KB0 + s * (uint64_t)KP;
+    MidRes mr;
+    mr.x = lds.mid_x;
+    mr.inc = lds.mid_inc;
+    mr.have = __builtin_amdgcn_readfirstlane(lds.x_seg) == g_seg;
     // One dynamic queue over both lists, interleaved (list 1 at even, list 2
     // at odd positions while both last). Claims run two units ahead: the LDS
     // atomic for unit j+2 is issued when unit j starts and read when it ends
@@ -1080,17 +1134,17 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
           const uint32_t p = pi & 0xFFFFu;
           const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mid_m[k] >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_mid_m[k]);
-          if ((uint64_t)p * p < Vend) unit_A(img0, pi, m, Vs, rg.rho_pack, lane, one);
+          if ((uint64_t)p * p < Vend) unit_A(img0, pi, m, mr, k, Vs, rg.rho_pack, lane, one);
         } else if (k < nA + nB1) {
           const uint32_t j0 = nA + (k - nA) * 2;
           const uint32_t pf = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
           if ((uint64_t)pf * pf < Vend)
-            unit_B1(img0, s_mid_p, s_mid_m, j0, min(2u, n_b1 - j0), Vs, rg.rho_pack, lane, one);
+            unit_B1(img0, s_mid_p, s_mid_m, mr, j0, min(2u, n_b1 - j0), Vs, rg.rho_pack, lane, one);
         } else {
           const uint32_t j0 = n_b1 + (k - nA - nB1) * 8;
           const uint32_t pf = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
           if ((uint64_t)pf * pf < Vend)
-            unit_B2(img0, s_mid_p, s_mid_m, j0, min(8u, n_mid - j0), Vs, Vend, rg.rho_pack, lane, one);
+            unit_B2(img0, s_mid_p, s_mid_m, mr, j0, min(8u, n_mid - j0), Vs, Vend, rg.rho_pack, lane, one);
         }
       } else {
         const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p);
@@ -1117,7 +1171,14 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     // expanded: no barrier in between, and waves drift into init while
     // others still expand
     if (t + 1 < T) init_segment(lds.img, s + grid);
-    if (tid == 0) lds.ctr = 0;  // all claims of this segment returned before the barrier above
+    if (tid == 0) {
+      lds.ctr = 0;  // all claims of this segment returned before the barrier above
+      // the mid units left their residues for segment s + grid: valid if it is
+      // of the same range and every mid unit ran (p^2 < Vs for p <= TB)
+      const uint32_t r0 = range_of(s), r1 = range_of(s + grid);
+      const uint64_t Vs = wa.r[r0].V0 + (uint64_t)(s - wa.r[r0].seg0) * kWheelSpan;
+      lds.x_seg = t + 1 < T && r1 == r0 && Vs >= (uint64_t)TB * TB ? s + grid : ~0u;
+    }
     __syncthreads();
   }
 
