@@ -162,22 +162,21 @@ def lds_instr_check(wm: int, cs: int, pmc):
     """The analytic executed-mark count against the PMC's LDS wave-instructions
     per launch: SQ_INSTS_LDS = the marks (wm / 64 full-wave ds_or_b32) + the
     expansion and init instructions, which the kernel's structure fixes per
-    segment (expand: 2 ds_read_b128 + 32 LUT ds_read_b32 per lane-row, 4,096
-    lane-rows; init: 7 x 9 ds_read_b128 table reads + 32 ds_write_b32 per lane,
-    1,024 lanes; csrc/dse_wheel.hip expand_segment / init_segment) + a rest:
-    unit claims and the ds_or of predicated marks issued with part of the wave
-    (A-class and B tails, L planes with <= 2 hits), which the analytic count
-    of hits cannot see: ~2.3 K wave-instructions per segment at N=1e11
-    (DESIGN.md section 6), 9-11% of the total. A negative rest, or one far above
-    that, would mean the analytic count is off. (A half-geometry tail segment
-    has half the lane-rows and 51 instead of 95 init instructions per lane:
-    counted here as full segments, < 0.1% at N=1e11.)"""
+    segment (expand: 2 ds_read_b128 + 32 LUT ds_read_b32 per lane-block, 4,096
+    blocks; init: 7 x (5 + 5 + 1) ds_read_b128 table reads + 33 ds_write_b32
+    per lane, 1,024 lanes; csrc/dse_wheel.hip expand_segment / init_segment) +
+    a rest: unit claims, the mid-prime residue reads and writes, and the ds_or
+    of predicated marks issued with part of the wave (A-class and B tails, L
+    planes with <= 2 hits), which the analytic count of hits cannot see. A
+    negative rest, or one far above ~10%, would mean the analytic count is
+    off. (A half-geometry tail segment has half the blocks and fewer init
+    instructions per lane: counted here as full segments, < 0.1% at N=1e11.)"""
     if not pmc:
         return None
     nseg = -(-cs // work.WHEEL_OUT_BITS)
     mark_i = wm / 64
     expand_i = nseg * (4096 // 64) * 34
-    init_i = nseg * (1024 // 64) * (7 * 9 + 32)
+    init_i = nseg * (1024 // 64) * (7 * 11 + 33)
     rest = pmc["sq_insts_lds"] - mark_i - expand_i - init_i
     return {"sq_insts_lds": pmc["sq_insts_lds"], "marks_analytic": mark_i, "expand": expand_i, "init": init_i,
             "rest": rest, "rest_share": rest / pmc["sq_insts_lds"],

@@ -1,7 +1,15 @@
-# Round-4 evidence of the in-tree build: rocprofv3 trace + PMC of the default bench (tools/profile.sh),
-# the extra PMC pass groups (tools/gpu/pmc_deep.sh), per-chunk costs of the multi-chunk configs.
+# Round-4 evidence of the in-tree build: GPU tests, the default bench line (CPU baseline included),
+# rocprofv3 trace + PMC of the bench (tools/profile.sh), the extra PMC groups (tools/gpu/pmc_deep.sh),
+# per-chunk costs of the multi-chunk configs + the 1-GPU config sweep, window kernel stats.
 set -o pipefail
+O=gpurun_out/ev
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputest.log 2>&1 || { tail -40 $O/gputest.log; exit 1; }
+tail -1 $O/gputest.log
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python3 -c "import json; j=json.load(open('$O/bench.json')); print('bench', j['ms_per_step'], j['value'], j['verified'], j['roofline']['kernel_ms'], j['cpu_baseline']['value'])"
 timeout -k 10 600 bash tools/profile.sh r04 || exit 1
 OUT=gpurun_out/pmc_deep N=1e11 bash tools/gpu/pmc_deep.sh > /dev/null 2>&1 || exit 1
-tail -30 gpurun_out/pmc_deep/summary.txt
+tail -22 gpurun_out/pmc_deep/summary.txt
 OUT=gpurun_out/rank_steps bash tools/gpu/rank_steps_all.sh || exit 1
+bash tools/gpu/window_kstats.sh || exit 1
