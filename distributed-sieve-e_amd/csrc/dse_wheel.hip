@@ -243,16 +243,39 @@ __device__ __forceinline__ void mark_k_step(uint32_t pb4, uint32_t& k, uint32_t 
       : "memory");
 }
 
-// n unconditional marks k, k + p, ... (unrolled by 4 by hand: three SALU of
-// loop control per mark otherwise); returns the index after the run.
+// Four mark_k_steps in one asm block. Between two asm blocks the compiler
+// puts a wait state (s_nop 0, or a filler) whenever the second reads a VGPR
+// the first wrote -- it cannot see that no instruction in them needs one --
+// so back-to-back mark_k_steps cost an s_nop per mark.
+__device__ __forceinline__ void mark_k_step4(uint32_t pb4, uint32_t& k, uint32_t p, uint32_t one) {
+  uint32_t a0, b0, a1, b1;
+  asm volatile(
+      "v_and_or_b32 %0, %4, %5, %6\n\t"
+      "v_lshlrev_b32 %1, %4, %8\n\t"
+      "v_add_u32 %4, %4, %7\n\t"
+      "ds_or_b32 %0, %1\n\t"
+      "v_and_or_b32 %2, %4, %5, %6\n\t"
+      "v_lshlrev_b32 %3, %4, %8\n\t"
+      "v_add_u32 %4, %4, %7\n\t"
+      "ds_or_b32 %2, %3\n\t"
+      "v_and_or_b32 %0, %4, %5, %6\n\t"
+      "v_lshlrev_b32 %1, %4, %8\n\t"
+      "v_add_u32 %4, %4, %7\n\t"
+      "ds_or_b32 %0, %1\n\t"
+      "v_and_or_b32 %2, %4, %5, %6\n\t"
+      "v_lshlrev_b32 %3, %4, %8\n\t"
+      "v_add_u32 %4, %4, %7\n\t"
+      "ds_or_b32 %2, %3"
+      : "=&v"(a0), "=&v"(b0), "=&v"(a1), "=&v"(b1), "+v"(k)
+      : "s"(kBlockMask), "v"(pb4), "v"(p), "v"(one)
+      : "memory");
+}
+
+// n unconditional marks k, k + p, ... (by 4: three SALU of loop control per
+// mark otherwise); returns the index after the run.
 __device__ __forceinline__ uint32_t mark_run(uint32_t pb4, uint32_t k, uint32_t p, uint32_t n, uint32_t one) {
   uint32_t h = 0;
-  for (; h + 4 <= n; h += 4) {
-    mark_k_step(pb4, k, p, one);
-    mark_k_step(pb4, k, p, one);
-    mark_k_step(pb4, k, p, one);
-    mark_k_step(pb4, k, p, one);
-  }
+  for (; h + 4 <= n; h += 4) mark_k_step4(pb4, k, p, one);
   for (; h < n; ++h) mark_k_step(pb4, k, p, one);
   return k;
 }
@@ -617,23 +640,64 @@ __device__ __forceinline__ uint32_t plane_start(uint32_t a, uint32_t nKbm, uint3
 // (the common case): the mark count per plane is decided once per unit.
 // MODE 2: pmin > KP, one predicated mark per plane; MODE 1: pmin > KP/2, two;
 // MODE 0: n_min unconditional marks per plane and a short loop for the rest.
+// A plane start and its NM = 1 or 2 predicated marks kk, kk + p in one block
+// (separate blocks cost a wait state between them, mark_k_step4); the second
+// mark's lanes are a subset of the first's, so exec is narrowed twice and
+// restored once, from sv (the unit's exec, saved once). 7 (11) VALU + 1 SALU.
+template <int NM>
+__device__ __forceinline__ void start_marks(uint32_t a, uint32_t nKbm, uint32_t ne, uint32_t p, uint32_t pb4,
+                                            uint32_t one, uint64_t sv) {
+  uint32_t t, u, b;
+  if (NM == 1)
+    asm volatile(
+        "v_add3_u32 %0, %3, %4, %5\n\t"
+        "v_add_u32 %1, %0, %6\n\t"
+        "v_min_u32 %0, %0, %1\n\t"
+        "v_and_or_b32 %1, %0, %8, %9\n\t"
+        "v_lshlrev_b32 %2, %0, %10\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %7, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %11"
+        : "=&v"(t), "=&v"(u), "=&v"(b)
+        : "v"(a), "v"(nKbm), "v"(ne), "v"(p), "s"(KP), "s"(kBlockMask), "v"(pb4), "v"(one), "s"(sv)
+        : "memory", "vcc");
+  else
+    asm volatile(
+        "v_add3_u32 %0, %3, %4, %5\n\t"
+        "v_add_u32 %1, %0, %6\n\t"
+        "v_min_u32 %0, %0, %1\n\t"
+        "v_and_or_b32 %1, %0, %8, %9\n\t"
+        "v_lshlrev_b32 %2, %0, %10\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %7, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "v_add_u32 %0, %0, %6\n\t"
+        "v_and_or_b32 %1, %0, %8, %9\n\t"
+        "v_lshlrev_b32 %2, %0, %10\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %7, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %11"
+        : "=&v"(t), "=&v"(u), "=&v"(b)
+        : "v"(a), "v"(nKbm), "v"(ne), "v"(p), "s"(KP), "s"(kBlockMask), "v"(pb4), "v"(one), "s"(sv)
+        : "memory", "vcc");
+}
+
 template <int MODE>
 __device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, const PlaneSteps& ps,
                                             uint32_t n_min) {
   const uint32_t p = o.p;
+  if (MODE != 0) {  // 1e11: SALU -5.6%, time +-0 (profiles/r04/ab_exec_once_*.txt)
+    uint64_t sv;
+    asm volatile("s_mov_b64 %0, exec" : "=s"(sv));
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) start_marks<MODE == 1 ? 2 : 1>(o.a[q], nKbm, ps.ne[q], p, ps.pb[q], ps.one, sv);
+    return;
+  }
 #pragma unroll
   for (uint32_t q = 0; q < 8; ++q) {
     uint32_t kk = plane_start(o.a[q], nKbm, ps.ne[q], p);
     const uint32_t pb4 = ps.pb[q];
-    if (MODE == 2) {
-      mark_plane<true>(pb4, kk, ps.one);
-    } else if (MODE == 1) {
-      mark_plane<true>(pb4, kk, ps.one);
-      mark_plane<true>(pb4, kk + p, ps.one);
-    } else {
-      kk = mark_run(pb4, kk, p, n_min, ps.one);
-      for (; kk < KP; kk += p) mark_plane<false>(pb4, kk, ps.one);  // a predicated fixed-count tail is slower
-    }
+    kk = mark_run(pb4, kk, p, n_min, ps.one);
+    for (; kk < KP; kk += p) mark_plane<false>(pb4, kk, ps.one);  // a predicated fixed-count tail is slower
   }
 }
 
