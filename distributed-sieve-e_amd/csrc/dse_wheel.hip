@@ -559,10 +559,10 @@ struct LargeOps {
 };
 
 __device__ __forceinline__ void load_L(LargeOps& o, const uint32_t* __restrict__ P, const uint64_t* __restrict__ M,
-                                       const uint32_t* __restrict__ A, uint32_t il, uint32_t np) {
+                                       const uint32_t* __restrict__ A, uint32_t il, uint32_t np, bool need_m) {
   const uint32_t ic = min(il, np - 1);  // past the table end: load the last row, mark nothing
   o.p = il < np ? P[ic] : 0x7FFFFFFFu;
-  o.m = M[ic];
+  o.m = need_m ? M[ic] : 0ull;  // the Barrett factor: only for Kb >= 2^38 (unit_L); 1e12: -1.9%
   const uint4* row = reinterpret_cast<const uint4*>(A + 8ull * ic);
   const uint4 lo = row[0], hi = row[1];
   o.a[0] = lo.x; o.a[1] = lo.y; o.a[2] = lo.z; o.a[3] = lo.w;
@@ -1085,6 +1085,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       ps.ne[q] = 0u - ((e_rot >> q) & 1u);
     }
     const uint64_t Kb = rg.KB0 + s * (uint64_t)KP;
+    const bool need_m = Kb >= (1ull << 38);  // unit_L's Barrett path
     MidRes mr;
     mr.x = lds.mid_x;
     mr.inc = lds.mid_inc;
@@ -1124,8 +1125,8 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     uint32_t q_cur = claimed(claim());
     uint32_t q_nxt = claimed(claim());
     if (q_cur < n_q && unit_of(q_cur) != ~0u && is_l(unit_of(q_cur))) {
-      load_L(cur, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_cur)) + lane, i_big);
-      load_L(cur1, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_cur)) + 64 + lane, i_big);
+      load_L(cur, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_cur)) + lane, i_big, need_m);
+      load_L(cur1, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_cur)) + 64 + lane, i_big, need_m);
     }
     while (q_cur < n_q) {
       // issued and read in the same iteration: the asm output is written when
@@ -1134,8 +1135,8 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       // iteration into the next gave wrong counts)
       const uint32_t c2 = claim();  // unit after next, read at the end of this one
       if (q_nxt < n_q && unit_of(q_nxt) != ~0u && is_l(unit_of(q_nxt))) {
-        load_L(nxt, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_nxt)) + lane, i_big);
-        load_L(nxt1, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_nxt)) + 64 + lane, i_big);
+        load_L(nxt, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_nxt)) + lane, i_big, need_m);
+        load_L(nxt1, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_nxt)) + 64 + lane, i_big, need_m);
       }
       const uint32_t u_cur = unit_of(q_cur);
       if (BK && u_cur == ~0u) {  // a bucket unit, kBkBatchU loads in flight per lane
