@@ -59,6 +59,9 @@ def parse():
     ap.add_argument("--no-mask", action="store_true", help="count only (not the product path; diagnostics)")
     ap.add_argument("--cpu-baseline", choices=["on", "off"], default="on")
     ap.add_argument("--cpu-max-n", type=float, default=1e8, help="largest N of the CPU baseline runs")
+    ap.add_argument("--rccl-single", action="store_true",
+                    help="one GPU only: form a 1-rank nccl (RCCL) process group and run the step's broadcast and "
+                         "all-reduce through it, as every rank of an N-GPU run does (exercises the RCCL path)")
     return ap.parse_args()
 
 
@@ -193,11 +196,17 @@ def main():
     rehearse = os.environ.get("DSE_BENCH_REHEARSE") == "1"
     if rehearse:
         local = 0
+    if a.rccl_single and world != 1:
+        sys.exit("--rccl-single is for a one-process run")
+    pg = world > 1 or a.rccl_single  # the step's collectives run through a process group
     if world > 1:
         if rehearse:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif a.rccl_single:
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1,
+                                device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     P = world  # one spread-work chunk (or window slice) per GPU
@@ -226,8 +235,8 @@ def main():
     if world > 1:
         ranks = [None] * world
         dist.all_gather_object(ranks, me)
-    world_info = {"backend": dist.get_backend() if world > 1 else None, "size": world, "ranks": ranks,
-                  "rehearsal": rehearse}
+    world_info = {"backend": dist.get_backend() if pg else None, "size": world, "ranks": ranks,
+                  "rehearsal": rehearse, "rccl_single": a.rccl_single}
 
     ctx = S.Context(device=local)
     tbytes = S.base_table_bytes(limit)
@@ -243,7 +252,7 @@ def main():
         counts.zero_()
         if rank == 0:
             ctx.base_primes_dev_async(limit, table.data_ptr(), tbytes, sp)
-        if world > 1:
+        if pg:
             dist.broadcast(table[:pbytes], src=0)
             if rank != 0:
                 ctx.base_table_finish_dev_async(limit, table.data_ptr(), tbytes, sp)
@@ -257,7 +266,7 @@ def main():
             kev.append(e)
         if rank == world - 1 and tail_n:
             ctx.sieve_range_dev_async(table.data_ptr(), tail_g, tail_n, 0, counts.data_ptr() + 8, sp)
-        if world > 1:
+        if pg:
             dist.all_reduce(counts)
 
     def step(timed=False):
@@ -396,7 +405,7 @@ def main():
             out["cpu_baseline"] = cpu_baseline(int(a.cpu_max_n))
         print(json.dumps(out), flush=True)
     ctx.close()
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
 
 

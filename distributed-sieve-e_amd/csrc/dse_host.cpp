@@ -91,6 +91,11 @@ struct dse_ctx {
   // dse_debug_init_logical: every DevState on device 0, the collectives
   // replaced by copies (xfer_table / allreduce_counts); on device 0:
   bool logical = false;
+  // dse_debug_set_option("rccl_single"): a one-device context with a 1-rank
+  // RCCL communicator, so share_table / allreduce_counts issue the real
+  // grouped ncclBroadcast / ncclAllReduce on a one-GPU box.
+  bool rccl_single = false;
+  int64_t rccl_calls = 0;                  // collectives RCCL accepted (dse_debug_get_stat)
   unsigned long long* lg_stage = nullptr;  // gathered counts [devs][n]
   unsigned long long* lg_sum = nullptr;    // their sum [n]
   uint64_t lg_n = 0;                       // n of the two buffers
@@ -189,7 +194,7 @@ int32_t share_table(dse_ctx* ctx, uint64_t limit) {
   HIP_TRY(hipSetDevice(ctx->devs[0].device));
   if ((rc = build_table(ctx->devs[0], limit))) return rc;
   const int nd = (int)ctx->devs.size();
-  if (nd == 1) return DSE_OK;
+  if (nd == 1 && !ctx->rccl_single) return DSE_OK;
   const uint64_t pbytes = dse_base_table_prime_bytes(limit);
   if (ctx->logical) {  // the broadcast as copies from device 0's table, each on its device's stream
     DevState& r = ctx->devs[0];
@@ -208,6 +213,7 @@ int32_t share_table(dse_ctx* ctx, uint64_t limit) {
     NCCL_TRY(ncclBroadcast(ctx->devs[0].table, d.table, pbytes, ncclUint8, 0, ctx->comms[i], d.stream));
   }
   NCCL_TRY(ncclGroupEnd());
+  ctx->rccl_calls += nd;
   for (int i = 1; i < nd; ++i) {
     DevState& d = ctx->devs[i];
     HIP_TRY(hipSetDevice(d.device));
@@ -218,7 +224,7 @@ int32_t share_table(dse_ctx* ctx, uint64_t limit) {
 
 // Sum `n` uint64 counts over the devices with an RCCL all-reduce (in place).
 int32_t allreduce_counts(dse_ctx* ctx, uint64_t n) {
-  if (ctx->devs.size() < 2) return DSE_OK;
+  if (ctx->devs.size() < 2 && !ctx->rccl_single) return DSE_OK;
   if (ctx->logical) {  // gather + sum on device 0's stream, then every device copies the sum back
     const uint32_t nd = (uint32_t)ctx->devs.size();
     DevState& r = ctx->devs[0];
@@ -257,6 +263,7 @@ int32_t allreduce_counts(dse_ctx* ctx, uint64_t n) {
     NCCL_TRY(ncclAllReduce(d.counts, d.counts, n, ncclUint64, ncclSum, ctx->comms[i], d.stream));
   }
   NCCL_TRY(ncclGroupEnd());
+  ctx->rccl_calls += (int64_t)ctx->devs.size();
   return DSE_OK;
 }
 
@@ -522,7 +529,8 @@ int32_t dse_sieve_all(dse_ctx* ctx, int64_t n, int32_t P, uint64_t* per_chunk_co
   for (int i = 0; i < nd; ++i) {
     DevState& d = ctx->devs[i];
     HIP_TRY(hipSetDevice(d.device));
-    bool reuse = ctx->last_n >= 0 && ctx->last_P == P && !d.resident.empty() && d.resident[0].words == words;
+    // the same (n, P) as the last call: the same chunk map and mask sizes
+    const bool reuse = ctx->last_n == n && ctx->last_P == P && !d.resident.empty() && d.resident[0].words == words;
     if (!reuse) {
       if ((rc = free_resident(d))) return rc;
       for (int32_t k = i + 1; k <= P; k += nd) {
@@ -532,8 +540,6 @@ int32_t dse_sieve_all(dse_ctx* ctx, int64_t n, int32_t P, uint64_t* per_chunk_co
         HIP_TRY(hipMalloc(&cm.dev_ptr, words * 8));
         d.resident.push_back(cm);
       }
-    } else {
-      for (auto& cm : d.resident) cm.my_num = cm.my_num;  // same layout as last call
     }
     if ((rc = ensure_table(d, limit))) return rc;
     if ((rc = ensure_counts(d, nc))) return rc;
@@ -693,12 +699,51 @@ int32_t dse_debug_set_option(dse_ctx* ctx, const char* name, int64_t value) {
     ctx->opts.scratch_poison = (uint32_t)value;
     return DSE_OK;
   }
+  if (n == "rccl_single") {
+    if (value < 0 || value > 1) return fail(DSE_EINVAL, "rccl_single must be 0 or 1");
+    if (ctx->logical || ctx->devs.size() != 1)
+      return fail(DSE_EINVAL, "rccl_single needs a one-device context (dse_init(1) or dse_init_device)");
+    if (value == 1 && ctx->comms.empty()) {
+      int dev = ctx->devs[0].device;
+      HIP_TRY(hipSetDevice(dev));
+      ncclComm_t c;
+      NCCL_TRY(ncclCommInitAll(&c, 1, &dev));
+      ctx->comms.push_back(c);
+    } else if (value == 0 && !ctx->comms.empty()) {
+      HIP_TRY(hipSetDevice(ctx->devs[0].device));
+      HIP_TRY(hipStreamSynchronize(ctx->devs[0].stream));
+      NCCL_TRY(ncclCommDestroy(ctx->comms[0]));
+      ctx->comms.clear();
+    }
+    ctx->rccl_single = value == 1;
+    return DSE_OK;
+  }
   if (n == "bucket_cap_divisor") {
     if (value < 0 || value > 0xFFFFFFFFll) return fail(DSE_EINVAL, "bucket_cap_divisor out of range");
     ctx->opts.bucket_cap_div = (uint32_t)value;
     return DSE_OK;
   }
   return fail(DSE_EINVAL, "unknown option " + n);
+}
+
+int32_t dse_debug_get_stat(dse_ctx* ctx, const char* name, int64_t* value) {
+  if (!ctx || !name || !value) return fail(DSE_EINVAL, "null ctx, stat name or value");
+  const std::string n(name);
+  if (n == "rccl_calls") {
+    *value = ctx->rccl_calls;
+    return DSE_OK;
+  }
+  if (n == "rccl_comms") {
+    *value = (int64_t)ctx->comms.size();
+    return DSE_OK;
+  }
+  if (n == "rccl_ranks") {  // ranks of the context's communicators, as RCCL reports them
+    int c = 0;
+    if (!ctx->comms.empty()) NCCL_TRY(ncclCommCount(ctx->comms[0], &c));
+    *value = c;
+    return DSE_OK;
+  }
+  return fail(DSE_EINVAL, "unknown stat " + n);
 }
 
 }  // extern "C"

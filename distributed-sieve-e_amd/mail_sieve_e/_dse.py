@@ -56,6 +56,7 @@ SIGNATURES = {
     "dse_device_status": (_i32, [_vp]),
     "dse_debug_set_option": (_i32, [_vp, _cp, _i64]),
     "dse_debug_init_logical": (_vp, [_i32]),
+    "dse_debug_get_stat": (_i32, [_vp, _cp, _pi64]),
 }
 
 _lib = None

@@ -112,6 +112,12 @@ class Context:
         """Test-only knob of this context (include/dse.h dse_debug_set_option)."""
         check(lib().dse_debug_set_option(self.ptr, name.encode(), int(value)), "dse_debug_set_option")
 
+    def debug_get_stat(self, name: str) -> int:
+        """Test-only statistic of this context (include/dse.h dse_debug_get_stat)."""
+        v = ctypes.c_int64(0)
+        check(lib().dse_debug_get_stat(self.ptr, name.encode(), ctypes.byref(v)), "dse_debug_get_stat")
+        return v.value
+
     # -- device-buffer entry points (torch tensors' data_ptr()) --------------
     def base_primes_dev_async(self, limit: int, table_ptr: int, table_bytes: int, stream_ptr: int = 0):
         check(lib().dse_base_primes_dev_async(self.ptr, limit, table_ptr, table_bytes, stream_ptr or None),

@@ -196,11 +196,25 @@ int32_t dse_device_status(dse_ctx *ctx);
  *   "scratch_poison" = 1: fill the bucket scratch with 0xFF bytes before
  *   every bucketed pass (stale contents: results unchanged, and an overflowed
  *   pass still reads only what it wrote); 0 = default.
+ *   "rccl_single" = 1: give a one-device context (dse_init(1) or
+ *   dse_init_device) a 1-rank RCCL communicator (ncclCommInitAll), so
+ *   dse_sieve_all / dse_sieve_window issue the same grouped ncclBroadcast of
+ *   the primes and ncclAllReduce of the counts as an 8-GPU context instead of
+ *   skipping them (the RCCL path exercised on a one-GPU box); 0 = default (no
+ *   communicator, no collective for one device).
  * DSE_EINVAL for an unknown name or a value out of range. */
 int32_t dse_debug_set_option(dse_ctx *ctx, const char *name, int64_t value);
 
+/* Read a test-only statistic of this context into *value:
+ *   "rccl_calls": RCCL collectives (one per device and call) accepted so far;
+ *   "rccl_comms": communicators the context holds;
+ *   "rccl_ranks": ranks of its communicator as ncclCommCount reports (0: none).
+ * DSE_EINVAL for an unknown name. */
+int32_t dse_debug_get_stat(dse_ctx *ctx, const char *name, int64_t *value);
+
 /* A context of num_logical devices that all run on device 0 (each its own
- * stream, table, counts, masks, scratch and side streams), so the multi-device
+ * stream, table, counts, masks and scratch; a device's chunks are pooled into
+ * one persistent launch, as on a real device), so the multi-device
  * code of dse_sieve_all / dse_sieve_window -- chunk map, table completion on
  * the non-root devices, tail on the last device, flag checks -- runs on a
  * one-GPU box. Only the two RCCL collectives are replaced: the broadcast of

@@ -84,3 +84,19 @@ def test_bench_two_rank_rehearsal():
     d = _last_json(r.stdout)
     _check_line(d, 2)
     assert d["config"]["P"] == 2 and d["pi_full"] == 455052511
+
+
+@pytest.mark.gpu
+def test_bench_single_rank_rccl_line():
+    """--rccl-single: the step's dist.broadcast of the primes and dist.all_reduce
+    of the counts run through a real 1-rank nccl (RCCL) process group, formed
+    by the same init_process_group("nccl", device_id=...) call an N-GPU rank
+    makes; pi stays verified and the line names the nccl backend."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--n", "1e10", "--steps", "3", "--warmup", "1",
+                        "--cpu-baseline", "off", "--rccl-single"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _last_json(r.stdout)
+    _check_line(d, 1)
+    assert d["world"]["backend"] == "nccl" and d["world"]["rccl_single"] is True
+    assert d["pi_full"] == 455052511

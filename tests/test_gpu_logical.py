@@ -2,14 +2,15 @@
 
 dse_debug_init_logical(k) (include/dse.h) builds a context of k logical
 devices that all run on device 0, each with its own stream, table, counts,
-resident masks, scratch and side streams; only the two RCCL collectives are
+resident masks and scratch; only the two RCCL collectives are
 replaced (the prime broadcast by device-to-device copies of device 0's table,
 the count all-reduce by a gather + sum on device 0 and a copy back, each
 ordered with events where the RCCL calls sit). So the chunk map of
 sieve.clj:24-34 over devices (chunk k on device (k-1) mod k_dev), the table
 completion on the non-root devices (dse_base_table_finish: Barrett factors and
-wheel offsets derived locally), the tail on the last device, side streams for
-several chunks per device, window slices and the per-device flag checks all
+wheel offsets derived locally), the tail on the last device, several chunks
+of a device pooled into one persistent launch, window slices and the
+per-device flag checks all
 run here against the golden fixtures -- what dse_init(8) runs on an 8-GPU
 node, collectives aside.
 """
@@ -37,8 +38,9 @@ def S():
 @pytest.mark.parametrize("P,ndev", [(2, 2), (4, 4), (8, 8), (8, 3), (4, 8)])
 def test_1e10_golden_on_logical_devices(S, P, ndev):
     """BASELINE config 3 (N=1e10 over 2/4/8 GPUs): one chunk per device as on
-    a P-GPU node, and the uneven maps (8 chunks on 3 devices: side streams;
-    4 chunks on 8 devices: idle devices)."""
+    a P-GPU node, and the uneven maps (8 chunks on 3 devices: several chunks
+    pooled into one persistent launch per device; 4 chunks on 8 devices: idle
+    devices)."""
     g = GOLDEN["big"][f"1e10_P{P}"]
     with S.Context(logical=ndev) as c:
         assert c.num_devices == ndev
