@@ -92,6 +92,7 @@ constexpr uint32_t TB1 = DSE_TB1;           // B1/B2 threshold
 #endif
 constexpr uint32_t TB = DSE_TB;             // B2/L threshold
 static_assert(TA <= 256 && TA < TB1 && TB1 <= TB && TB <= KP / 8, "unit thresholds");
+static_assert(KP / (128 * (TA + 1)) <= 10 && KP / (32 * (TB1 + 1)) <= 10, "class_marks_k covers K <= 10");
 constexpr uint32_t kMidCap = TB >= 16384 ? 1920 : TB >= 8192 ? 1040 : TB >= 4096 ? 580 : 320;  // odd primes in (61, TB]
 constexpr uint32_t kOutWordsPerSeg = (uint32_t)(kWheelOutBits / 32);  // 30720
 
@@ -283,6 +284,52 @@ __device__ __forceinline__ uint32_t mark_run(uint32_t pb4, uint32_t k, uint32_t 
 // ds_or_b32 at a precomputed LDS byte address.
 __device__ __forceinline__ void mark_at(uint32_t a, uint32_t bit) {
   asm volatile("ds_or_b32 %0, %1" : : "v"(a), "v"(bit) : "memory");
+}
+
+// The hits k + (r + 32 t) p, r = 0..31, t < K, of a lane that walks one
+// plane from k with step p: class r's hits sit D = 32 S p periods apart (S =
+// 1 for a lane that takes consecutive hits, 4 for B1's lanes, which take 32
+// of every 128), so they share their bit and their byte addresses step by D
+// (a period index is its block's byte address): 3 VALU of setup per class,
+// then one v_add per mark (mark_k_step: 3 VALU per mark).
+template <int K>
+__device__ __forceinline__ void class_marks(uint32_t pb4, uint32_t k, uint32_t p, uint32_t D, uint32_t one) {
+#pragma unroll 1
+  for (uint32_t r = 0; r < 32; ++r) {
+    uint32_t a, b;
+    asm volatile(
+        "v_and_or_b32 %0, %2, %3, %4\n\t"
+        "v_lshlrev_b32 %1, %2, %5\n\t"
+        "ds_or_b32 %0, %1"
+        : "=&v"(a), "=&v"(b)
+        : "v"(k), "s"(kBlockMask), "v"(pb4), "v"(one)
+        : "memory");
+#pragma unroll
+    for (int t = 1; t < K; ++t) {
+      a += D;
+      mark_at(a, b);
+    }
+    k = opaque(k + p);
+  }
+}
+// K wave-uniform in 1..10 (B1: floor(KP / 128 pmax), B2: floor(KP / 32
+// pmax); 0: nothing)
+__device__ __forceinline__ void class_marks_k(uint32_t K, uint32_t pb4, uint32_t k, uint32_t p, uint32_t D,
+                                              uint32_t one) {
+  switch (K) {
+    case 0: return;
+    case 1: class_marks<1>(pb4, k, p, D, one); return;
+    case 2: class_marks<2>(pb4, k, p, D, one); return;
+    case 3: class_marks<3>(pb4, k, p, D, one); return;
+    case 4: class_marks<4>(pb4, k, p, D, one); return;
+    case 5: class_marks<5>(pb4, k, p, D, one); return;
+    case 6: class_marks<6>(pb4, k, p, D, one); return;
+    case 7: class_marks<7>(pb4, k, p, D, one); return;
+    case 8: class_marks<8>(pb4, k, p, D, one); return;
+    case 9: class_marks<9>(pb4, k, p, D, one); return;
+    case 10: class_marks<10>(pb4, k, p, D, one); return;
+    default: __builtin_unreachable();
+  }
 }
 
 // x mod p for x < 2^63 with m = floor((2^64-1)/p).
@@ -477,9 +524,9 @@ __device__ __forceinline__ void unit_A(uint32_t img0, uint32_t pi, uint64_t m, c
 // B1: two mid primes (TA < p <= TB1), one per half-wave; lane (plane L & 7,
 // j = (L >> 3) & 3) owns the hits n with n mod 128 in [32j, 32j + 32), in
 // order: 32 marks k, k + p, ... then a jump of 96p. The four lanes of a plane
-// are 32p periods apart: distinct banks, as in A. Blocks of 128 hits every
-// lane fills are unrolled without a test; the last one, partly filled, is
-// marked with a per-lane count.
+// are 32p periods apart: distinct banks, as in A. The blocks of 128 hits
+// every lane fills are marked class by class (class_marks); the last one,
+// partly filled, in order with a per-lane count.
 __device__ __forceinline__ void unit_B1(uint32_t img0, const uint32_t* __restrict__ s_mid_p,
                                         const uint64_t* __restrict__ s_mid_m, const MidRes& mr, uint32_t j0,
                                         uint32_t nj, uint64_t Vs, uint64_t rho_pack, uint32_t lane, uint32_t one) {
@@ -503,13 +550,12 @@ __device__ __forceinline__ void unit_B1(uint32_t img0, const uint32_t* __restric
   }
   // blocks every lane of the wave fills: n < 128 (t + 1) <= floor(KP / pmax)
   const uint32_t pmax = __builtin_amdgcn_readlane(p, nj == 2 ? 32 : 0);  // the list ascends
+  // class by class (hits 32j + r + 128t, t < tf: 128p periods apart, one
+  // bit): 1 VALU per mark where walking them takes 3 (1e11: -0.9%)
   const uint32_t tf = (KP / pmax) / 128;  // wave-uniform (a scalar division)
   const uint32_t skip = 96 * p;
-#pragma unroll 1
-  for (uint32_t t = 0; t < tf; ++t) {
-    k = mark_run(pb4, k, p, 32, one);
-    k += skip;
-  }
+  class_marks_k(tf, pb4, k, p, 128 * p, one);
+  k += tf * (128 * p);
   // the rest: ceil((KP - k) / p) hits left in this lane's next blocks of 32
   while (k < KP) {
     const uint32_t left = div_ceil_small(KP - k, p, invp);
@@ -520,9 +566,10 @@ __device__ __forceinline__ void unit_B1(uint32_t img0, const uint32_t* __restric
 }
 
 // B2: 8 mid primes (TB1 < p <= TB) x 8 planes; lane (prime L >> 3, plane
-// L & 7) walks its plane's hits in order: n_u unconditional marks for every
-// lane, then a short per-lane tail. A plane's lanes hold different primes,
-// so their banks collide at random (the L pattern).
+// L & 7) marks its plane's hits: n_u unconditional marks for every lane (the
+// first 32 floor(n_u / 32) class by class, the rest in order), then a short
+// per-lane tail. A plane's lanes hold different primes, so their banks
+// collide at random (the L pattern).
 __device__ __forceinline__ void unit_B2(uint32_t img0, const uint32_t* __restrict__ s_mid_p,
                                         const uint64_t* __restrict__ s_mid_m, const MidRes& mr, uint32_t j0,
                                         uint32_t nj, uint64_t Vs, uint64_t Vend, uint64_t rho_pack, uint32_t lane,
@@ -545,7 +592,12 @@ __device__ __forceinline__ void unit_B2(uint32_t img0, const uint32_t* __restric
   // lanes past the batch end mark nothing (their unconditional marks would
   // land in another prime's plane)
   if (!valid) return;
-  k = mark_run(pb4, k, p, n_u, one);
+  // the first 32 K of the n_u unconditional hits class by class (hits r +
+  // 32t, t < K: 32p periods apart, one bit), the rest in order
+  const uint32_t K = n_u / 32;
+  class_marks_k(K, pb4, k, p, 32 * p, one);
+  k += K * (32 * p);
+  k = mark_run(pb4, k, p, n_u - 32 * K, one);
   for (; k < KP; k += p) mark_k(pb4, k, one);
 }
 
