@@ -166,7 +166,7 @@ def lds_instr_check(wm: int, cs: int, pmc):
     per launch: SQ_INSTS_LDS = the marks (wm / 64 full-wave ds_or_b32) + the
     expansion and init instructions, which the kernel's structure fixes per
     segment (expand: 2 ds_read_b128 + 32 LUT ds_read_b32 per lane-block, 4,096
-    blocks; init: 7 x (5 + 5 + 1) ds_read_b128 table reads + 33 ds_write_b32
+    blocks; init: 9 x (5 + 5 + 1) ds_read_b128 table reads + 33 ds_write_b32
     per lane, 1,024 lanes; csrc/dse_wheel.hip expand_segment / init_segment) +
     a rest: unit claims, the mid-prime residue reads and writes, and the ds_or
     of predicated marks issued with part of the wave (A-class and B tails, L
@@ -179,7 +179,7 @@ def lds_instr_check(wm: int, cs: int, pmc):
     nseg = -(-cs // work.WHEEL_OUT_BITS)
     mark_i = wm / 64
     expand_i = nseg * (4096 // 64) * 34
-    init_i = nseg * (1024 // 64) * (7 * 11 + 33)
+    init_i = nseg * (1024 // 64) * (work.WHEEL_PATTERN_GROUPS * 11 + 33)
     rest = pmc["sq_insts_lds"] - mark_i - expand_i - init_i
     return {"sq_insts_lds": pmc["sq_insts_lds"], "marks_analytic": mark_i, "expand": expand_i, "init": init_i,
             "rest": rest, "rest_share": rest / pmc["sq_insts_lds"],
@@ -363,7 +363,7 @@ def main():
                 "frac": achieved / work.LDS_OR_PEAK_GBS,
                 "traffic": pmc["traffic"] if pmc else None,
                 "traffic_source": f"committed PMC pass {pmc['source']} (not this run)" if pmc else None,
-                "basis": "executed ds_or_b32 marks (mod-30 wheel, primes > 61) x 4 B per kernel second against "
+                "basis": "executed ds_or_b32 marks (mod-30 wheel, primes > 79) x 4 B per kernel second against "
                          "the LDS store path (64 B/clk/CU); kernel time from HIP events on the launch stream",
                 "peak_ds_or": work.LDS_DS_OR_PEAK_GBS,
                 "frac_ds_or": achieved / work.LDS_DS_OR_PEAK_GBS,
@@ -381,7 +381,7 @@ def main():
                 "hbm_bytes_per_launch": rf["hbm_bytes"],
                 "hbm_frac_algorithmic": rf["hbm_bytes"] / ks / 1e9 / work.HBM_PEAK_GBS,
                 "executed_marks_source": "analytic (mail_sieve_e/work.py wheel_marks_for_range: multiples p*m >= p^2 "
-                                         "with gcd(m, 30) = 1 of the primes 61 < p <= sqrt(N)), cross-checked "
+                                         "with gcd(m, 30) = 1 of the primes 79 < p <= sqrt(N)), cross-checked "
                                          "against SQ_INSTS_LDS in pmc_committed.lds_instr_check",
                 # Read from the newest committed rocprofv3 PMC passes of this config
                 # (profiles/<round>/pmc_*_sieve_kernel.csv), NOT measured in this run;

@@ -699,6 +699,11 @@ int32_t dse_debug_set_option(dse_ctx* ctx, const char* name, int64_t value) {
     ctx->opts.scratch_poison = (uint32_t)value;
     return DSE_OK;
   }
+  if (n == "bucket_lo_log2") {
+    if (value != 0 && (value < 17 || value > 20)) return fail(DSE_EINVAL, "bucket_lo_log2 must be 0 or 17..20");
+    ctx->opts.bucket_lo_log2 = (uint32_t)value;
+    return DSE_OK;
+  }
   if (n == "rccl_single") {
     if (value < 0 || value > 1) return fail(DSE_EINVAL, "rccl_single must be 0 or 1");
     if (ctx->logical || ctx->devs.size() != 1)

@@ -43,9 +43,10 @@ constexpr uint32_t kR30[8] = {1, 7, 11, 13, 17, 19, 23, 29};
 constexpr int kWheelLogKP = DSE_WHEEL_LOG_KP;
 constexpr uint64_t kWheelSpan = 30ull << kWheelLogKP;   // integers per segment
 constexpr uint64_t kWheelOutBits = kWheelSpan / 2;      // odd candidates per segment
-// Base primes above this go through the bucketed pass (dse_wheel.hip).
+// Ranges with base primes above this go through the bucketed pass
+// (dse_wheel.hip), which then buckets every prime above 2^kBucketLoLog.
 #ifndef DSE_WHEEL_MAX_LOG
-#define DSE_WHEEL_MAX_LOG 20  // A/B builds only (window: 2^21 7.95 ms, 2^20 7.85, 2^19 8.30)
+#define DSE_WHEEL_MAX_LOG 20  // A/B builds only (r05 window: 2^22 7.25 ms, 2^21 6.11, 2^20 5.62, 2^19 5.49)
 #endif
 constexpr uint64_t kWheelMaxPrime = 1ull << DSE_WHEEL_MAX_LOG;
 
@@ -78,6 +79,7 @@ struct SieveOpts {
   uint32_t bucket_k0_div = 0;     // > 1: divide the band-0 region capacity, to test the spill list
   uint32_t wheel_geometry = 0;    // ranges without buckets: 0 auto (half-size tail), 1 full only, 2 half only
   uint32_t scratch_poison = 0;    // 1: fill the bucket scratch with 0xFF bytes before every pass (stale contents)
+  uint32_t bucket_lo_log2 = 0;    // k in 17..20: bucketed ranges bucket the primes above 2^k (0: production)
 };
 
 hipError_t launch_base_primes(uint64_t limit, void* table, uint32_t cap, hipStream_t stream);

@@ -96,7 +96,7 @@ static_assert(KP / (128 * (TA + 1)) <= 10 && KP / (32 * (TB1 + 1)) <= 10, "class
 constexpr uint32_t kMidCap = TB >= 16384 ? 1920 : TB >= 8192 ? 1040 : TB >= 4096 ? 580 : 320;  // odd primes in (61, TB]
 constexpr uint32_t kOutWordsPerSeg = (uint32_t)(kWheelOutBits / 32);  // 30720
 
-constexpr uint32_t kQMax = 61;  // the pattern primes are 7..61
+constexpr uint32_t kQMax = 79;  // the pattern primes are 7..79
 
 constexpr uint32_t inv30_const(uint32_t q) {
   for (uint32_t x = 1; x < q; ++x)
@@ -118,9 +118,11 @@ constexpr uint32_t inv30_const(uint32_t q) {
 #ifndef DSE_BK_UNIT_BATCHES
 #define DSE_BK_UNIT_BATCHES 4
 #endif
-constexpr int kNG = 7;
-constexpr uint32_t kGQ[kNG][3] = {{7, 11, 13}, {17, 19, 1}, {23, 29, 1}, {31, 37, 1},
-                                  {41, 43, 1}, {47, 53, 1}, {59, 61, 1}};
+// 7..61 in 7 groups until round 4; 67..79 as two more groups (1e11 -0.3%, 1e12
+// -0.7%: the init reads of two more strings cost less than A units for 4 primes)
+constexpr int kNG = 9;
+constexpr uint32_t kGQ[kNG][3] = {{7, 11, 13}, {17, 19, 1}, {23, 29, 1}, {31, 37, 1}, {41, 43, 1},
+                                  {47, 53, 1}, {59, 61, 1}, {67, 71, 1}, {73, 79, 1}};
 constexpr uint32_t gmod(int g) { return kGQ[g][0] * kGQ[g][1] * kGQ[g][2]; }
 constexpr uint32_t kInitWords = IMG_WORDS / NT;  // words one lane inits per segment (one plane of a block run)
 constexpr uint32_t kInitRun = 32 * kInitWords;    // their periods
@@ -133,7 +135,7 @@ constexpr uint32_t gbase(int g) { return g == 0 ? 0u : gbase(g - 1) + gdw(g - 1)
 constexpr uint32_t kGDW = gbase(kNG);  // dwords per copy (620)
 constexpr uint32_t kGInv30[kNG] = {inv30_const(gmod(0)), inv30_const(gmod(1)), inv30_const(gmod(2)),
                                    inv30_const(gmod(3)), inv30_const(gmod(4)), inv30_const(gmod(5)),
-                                   inv30_const(gmod(6))};
+                                   inv30_const(gmod(6)), inv30_const(gmod(7)), inv30_const(gmod(8))};
 
 // The init tables, built at compile time (a launch copies them into LDS):
 // copy k, group g, dword gbase(g) + j = bits [32 (j + k), 32 (j + k) + 32) of U_g.
@@ -169,7 +171,7 @@ struct WheelRange {
   unsigned long long* count;  // incremented by the range's prime count (device)
   uint32_t pl_pack;    // plane of absolute residue R30[j] in bits [3j, 3j+3)
   uint32_t e_iota;     // bit j: floor((V0 + rho)/30) = KB0 + 1 for the plane of R30[j]
-  uint32_t fix0;       // output word 0 bits of the primes 3..61 inside the range
+  uint64_t fix;        // output words 0, 1: bits of the primes 3..kQMax inside the range
   uint32_t seg0;       // first segment of the range in the launch
   uint16_t v0g[kNG];   // V0 mod M_G (init tables)
 };
@@ -279,6 +281,36 @@ __device__ __forceinline__ uint32_t mark_run(uint32_t pb4, uint32_t k, uint32_t 
   for (; h + 4 <= n; h += 4) mark_k_step4(pb4, k, p, one);
   for (; h < n; ++h) mark_k_step(pb4, k, p, one);
   return k;
+}
+
+// The rest of a lane's walk: k, k + p, ... while k < KP, as one asm loop
+// that narrows exec as lanes finish (v_cmpx) and restores it once: 4 VALU
+// and one branch per step (the compiler's loop keeps a mask of finished
+// lanes: 2 more SALU per step; 1e11 -0.3%). All exec writes are inside the
+// block. The branches only decide whether to run another step: exec only
+// narrows, every mark is predicated by the exec the v_cmpx left, and a step
+// run with an empty exec changes nothing, so even a branch that read exec
+// from before the v_cmpx could not mark anything wrong, only run one empty
+// step (and k grows by p every step, so the loop ends).
+__device__ __forceinline__ void mark_tail(uint32_t pb4, uint32_t k, uint32_t p, uint32_t one) {
+  uint64_t sv;
+  uint32_t a, b;
+  asm volatile(
+      "s_mov_b64 %3, exec\n\t"
+      "v_cmpx_gt_u32_e32 vcc, %5, %2\n\t"
+      "s_cbranch_execz 2f\n"
+      "1:\n\t"
+      "v_and_or_b32 %0, %2, %6, %7\n\t"
+      "v_lshlrev_b32 %1, %2, %8\n\t"
+      "v_add_u32 %2, %2, %4\n\t"
+      "ds_or_b32 %0, %1\n\t"
+      "v_cmpx_gt_u32_e32 vcc, %5, %2\n\t"
+      "s_cbranch_execnz 1b\n"
+      "2:\n\t"
+      "s_mov_b64 exec, %3"
+      : "=&v"(a), "=&v"(b), "+v"(k), "=&s"(sv)
+      : "v"(p), "s"(KP), "s"(kBlockMask), "v"(pb4), "v"(one)
+      : "memory", "vcc");
 }
 
 // ds_or_b32 at a precomputed LDS byte address.
@@ -598,7 +630,7 @@ __device__ __forceinline__ void unit_B2(uint32_t img0, const uint32_t* __restric
   class_marks_k(K, pb4, k, p, 32 * p, one);
   k += K * (32 * p);
   k = mark_run(pb4, k, p, n_u - 32 * K, one);
-  for (; k < KP; k += p) mark_k(pb4, k, one);
+  mark_tail(pb4, k, p, one);
 }
 
 // Operands of one large unit, loaded ahead of use. The table row of prime i
@@ -663,6 +695,13 @@ __device__ __forceinline__ void mark_entry(uint32_t img0, uint32_t e, uint32_t o
       : "memory");
 }
 
+// Kb mod p by float quotients (unit_L): p > TB bounds the quotients.
+constexpr uint64_t kQuotBits = 22;                                 // Kb < 2^32: q < 2^32 / (TB + 1) < 2^22
+constexpr uint64_t kQuotErr38 = (1ull << (38 - 22)) / (TB + 1) + 1;  // Kb < 2^38: |q error| < 2^16 / (TB + 1) + 1
+static_assert((1ull << 32) / (TB + 1) < (1ull << kQuotBits), "Kb < 2^32: float quotient within 1 (and < 2^24 for __umul24)");
+static_assert((kQuotErr38 + 2) * kWheelMaxPrime < (1ull << 31), "Kb < 2^38: the rest Kb - q p must be exact in int32");
+static_assert(kWheelMaxPrime < (1ull << 23), "__mul24 / __umul24 operands and float-exact p");
+
 // L: 64 large primes (p > TB), one per lane; at step q lane L handles the
 // absolute residue (q + L) & 7 (a half-wave spreads over all 8 planes). The
 // per-plane hit count is at most ceil(KP / pmin): units whose primes all
@@ -692,44 +731,116 @@ __device__ __forceinline__ uint32_t plane_start(uint32_t a, uint32_t nKbm, uint3
 // (the common case): the mark count per plane is decided once per unit.
 // MODE 2: pmin > KP, one predicated mark per plane; MODE 1: pmin > KP/2, two;
 // MODE 0: n_min unconditional marks per plane and a short loop for the rest.
-// A plane start and its NM = 1 or 2 predicated marks kk, kk + p in one block
-// (separate blocks cost a wait state between them, mark_k_step4); the second
-// mark's lanes are a subset of the first's, so exec is narrowed twice and
-// restored once, from sv (the unit's exec, saved once). 7 (11) VALU + 1 SALU.
+// MODE 1/2: four planes per block, each a plane start (a - Kb - e) mod p and
+// its NM = 1 or 2 predicated marks kk, kk + p; a plane's second mark's lanes
+// are a subset of its first's, so exec is narrowed twice and restored once
+// per plane, from the copy the block saved on entry. Every exec write is
+// inside the block, so no code the compiler places between blocks can run
+// with a narrowed exec. 6 (10) VALU + 1 SALU per plane (one plane per block,
+// the r04 form, adds an exec save and the compiler's s_nop between two asm
+// blocks per plane: 1e12 +0.7%).
 template <int NM>
-__device__ __forceinline__ void start_marks(uint32_t a, uint32_t nKbm, uint32_t ne, uint32_t p, uint32_t pb4,
-                                            uint32_t one, uint64_t sv) {
+__device__ __forceinline__ void start_marks4(const uint32_t* a, const uint32_t* ne, const uint32_t* pb, uint32_t nKbm,
+                                             uint32_t p, uint32_t one) {
   uint32_t t, u, b;
+  uint64_t sv;
   if (NM == 1)
     asm volatile(
-        "v_add3_u32 %0, %3, %4, %5\n\t"
-        "v_add_u32 %1, %0, %6\n\t"
+        "s_mov_b64 %3, exec\n\t"
+        "v_add3_u32 %0, %4, %16, %8\n\t"
+        "v_add_u32 %1, %0, %17\n\t"
         "v_min_u32 %0, %0, %1\n\t"
-        "v_and_or_b32 %1, %0, %8, %9\n\t"
-        "v_lshlrev_b32 %2, %0, %10\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %7, %0\n\t"
+        "v_and_or_b32 %1, %0, %19, %12\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
         "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %11"
-        : "=&v"(t), "=&v"(u), "=&v"(b)
-        : "v"(a), "v"(nKbm), "v"(ne), "v"(p), "s"(KP), "s"(kBlockMask), "v"(pb4), "v"(one), "s"(sv)
+        "s_mov_b64 exec, %3\n\t"
+        "v_add3_u32 %0, %5, %16, %9\n\t"
+        "v_add_u32 %1, %0, %17\n\t"
+        "v_min_u32 %0, %0, %1\n\t"
+        "v_and_or_b32 %1, %0, %19, %13\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %3\n\t"
+        "v_add3_u32 %0, %6, %16, %10\n\t"
+        "v_add_u32 %1, %0, %17\n\t"
+        "v_min_u32 %0, %0, %1\n\t"
+        "v_and_or_b32 %1, %0, %19, %14\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %3\n\t"
+        "v_add3_u32 %0, %7, %16, %11\n\t"
+        "v_add_u32 %1, %0, %17\n\t"
+        "v_min_u32 %0, %0, %1\n\t"
+        "v_and_or_b32 %1, %0, %19, %15\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %3"
+        : "=&v"(t), "=&v"(u), "=&v"(b), "=&s"(sv)
+        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(ne[0]), "v"(ne[1]), "v"(ne[2]), "v"(ne[3]), "v"(pb[0]),
+          "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(nKbm), "v"(p), "s"(KP), "s"(kBlockMask), "v"(one)
         : "memory", "vcc");
   else
     asm volatile(
-        "v_add3_u32 %0, %3, %4, %5\n\t"
-        "v_add_u32 %1, %0, %6\n\t"
+        "s_mov_b64 %3, exec\n\t"
+        "v_add3_u32 %0, %4, %16, %8\n\t"
+        "v_add_u32 %1, %0, %17\n\t"
         "v_min_u32 %0, %0, %1\n\t"
-        "v_and_or_b32 %1, %0, %8, %9\n\t"
-        "v_lshlrev_b32 %2, %0, %10\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %7, %0\n\t"
+        "v_and_or_b32 %1, %0, %19, %12\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
         "ds_or_b32 %1, %2\n\t"
-        "v_add_u32 %0, %0, %6\n\t"
-        "v_and_or_b32 %1, %0, %8, %9\n\t"
-        "v_lshlrev_b32 %2, %0, %10\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %7, %0\n\t"
+        "v_add_u32 %0, %0, %17\n\t"
+        "v_and_or_b32 %1, %0, %19, %12\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
         "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %11"
-        : "=&v"(t), "=&v"(u), "=&v"(b)
-        : "v"(a), "v"(nKbm), "v"(ne), "v"(p), "s"(KP), "s"(kBlockMask), "v"(pb4), "v"(one), "s"(sv)
+        "s_mov_b64 exec, %3\n\t"
+        "v_add3_u32 %0, %5, %16, %9\n\t"
+        "v_add_u32 %1, %0, %17\n\t"
+        "v_min_u32 %0, %0, %1\n\t"
+        "v_and_or_b32 %1, %0, %19, %13\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "v_add_u32 %0, %0, %17\n\t"
+        "v_and_or_b32 %1, %0, %19, %13\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %3\n\t"
+        "v_add3_u32 %0, %6, %16, %10\n\t"
+        "v_add_u32 %1, %0, %17\n\t"
+        "v_min_u32 %0, %0, %1\n\t"
+        "v_and_or_b32 %1, %0, %19, %14\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "v_add_u32 %0, %0, %17\n\t"
+        "v_and_or_b32 %1, %0, %19, %14\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %3\n\t"
+        "v_add3_u32 %0, %7, %16, %11\n\t"
+        "v_add_u32 %1, %0, %17\n\t"
+        "v_min_u32 %0, %0, %1\n\t"
+        "v_and_or_b32 %1, %0, %19, %15\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "v_add_u32 %0, %0, %17\n\t"
+        "v_and_or_b32 %1, %0, %19, %15\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %3"
+        : "=&v"(t), "=&v"(u), "=&v"(b), "=&s"(sv)
+        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(ne[0]), "v"(ne[1]), "v"(ne[2]), "v"(ne[3]), "v"(pb[0]),
+          "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(nKbm), "v"(p), "s"(KP), "s"(kBlockMask), "v"(one)
         : "memory", "vcc");
 }
 
@@ -737,11 +848,9 @@ template <int MODE>
 __device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, const PlaneSteps& ps,
                                             uint32_t n_min) {
   const uint32_t p = o.p;
-  if (MODE != 0) {  // 1e11: SALU -5.6%, time +-0 (profiles/r04/ab_exec_once_*.txt)
-    uint64_t sv;
-    asm volatile("s_mov_b64 %0, exec" : "=s"(sv));
-#pragma unroll
-    for (uint32_t q = 0; q < 8; ++q) start_marks<MODE == 1 ? 2 : 1>(o.a[q], nKbm, ps.ne[q], p, ps.pb[q], ps.one, sv);
+  if (MODE != 0) {
+    start_marks4<MODE == 1 ? 2 : 1>(o.a, ps.ne, ps.pb, nKbm, p, ps.one);
+    start_marks4<MODE == 1 ? 2 : 1>(o.a + 4, ps.ne + 4, ps.pb + 4, nKbm, p, ps.one);
     return;
   }
 #pragma unroll
@@ -749,22 +858,20 @@ __device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, co
     uint32_t kk = plane_start(o.a[q], nKbm, ps.ne[q], p);
     const uint32_t pb4 = ps.pb[q];
     kk = mark_run(pb4, kk, p, n_min, ps.one);
-    for (; kk < KP; kk += p) mark_plane<false>(pb4, kk, ps.one);  // a predicated fixed-count tail is slower
+    mark_tail(pb4, kk, p, ps.one);
   }
 }
 
 __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t Vend, uint64_t Kb,
                                        const PlaneSteps& ps, uint32_t pl_rot, uint64_t rho_pack) {
   const uint32_t p = o.p;
-  const uint64_t p2 = (uint64_t)p * p;
-  const bool live = p2 < Vend;
-  const bool slow = p2 > Vs;
   const float invp = fast_rcp((float)p);
   // Kb mod p. While Kb < 2^32 (values below 1.29e11; wave-uniform) a float
-  // quotient is within one of the true one (|error| < 0.11: Kb's rounding to
-  // float <= 128/p, the rcp and the product 2^-23 of q < 2^19 for p > TB),
-  // corrected by two unsigned min steps; the 64-bit Barrett reduction covers
-  // the rest.
+  // quotient is within one of the true one: its relative error is below
+  // 2^-22 (Kb rounded to float 2^-24, the rcp 2^-23, the product 2^-24) and
+  // q < 2^32 / p < 2^22 for p > TB (kQuotBits), so |error| < 1, and the
+  // truncation adds at most one more: Kb - q p is in (-p, 2p), corrected by
+  // two unsigned min steps; the 64-bit Barrett reduction covers Kb >= 2^38.
   uint32_t kbm;
   if (Kb < (1ull << 32)) {
     const uint32_t q = (uint32_t)((float)(uint32_t)Kb * invp);
@@ -772,10 +879,11 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
     x = min(x, x + p);
     kbm = min(x, x - p);
   } else if (Kb < (1ull << 38)) {
-    // values below 8.2e12: the float quotient of Kb is within 17 of the true
-    // one (relative error < 2^-22, Kb / p < 2^26), so Kb - q p is exact in 32
-    // bits (|.| < 18 p < 2^25); one more float quotient of that rest leaves
-    // it in (-p, p). 12 VALU where the 64-bit Barrett reduction takes ~24.
+    // values below 8.2e12: the float quotient of Kb is within kQuotErr38 of
+    // the true one (relative error < 2^-22, Kb / p < 2^38 / (TB + 1)), so
+    // Kb - q p is exact in 32 bits (|.| < (kQuotErr38 + 1) p < 2^31, asserted
+    // below); one more float quotient of that rest leaves it in (-p, 2p). 12
+    // VALU where the 64-bit Barrett reduction takes ~24.
     const uint32_t q = (uint32_t)((float)Kb * invp);
     const int32_t r = (int32_t)((uint32_t)Kb - q * p);
     const int32_t q2 = (int32_t)((float)r * invp);
@@ -788,7 +896,10 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
   const uint32_t nKbm = 0u - kbm;
   const uint32_t pmin = __builtin_amdgcn_readfirstlane(p);
   const uint32_t pmax = __builtin_amdgcn_readlane(p, 63);
-  const bool none = __builtin_amdgcn_ballot_w64(!live || slow) != 0;
+  // some lane not live or with p^2 inside the segment: the set's primes
+  // ascend (lanes past the table end hold 0x7FFFFFFF), so pmax decides, on
+  // the scalar unit (a per-lane 64-bit p^2 and two compares: 1e12 +1.4%)
+  const bool none = (uint64_t)pmax * pmax > Vs;
   const uint32_t n_min = (none || pmax >= KP) ? 0u : div_small(KP - pmax, pmax, fast_rcp((float)pmax));
   if (!none) {  // every lane live and past p^2: branch-free bodies
     if (pmin > KP) unit_L_fast<2>(o, nKbm, ps, 0);
@@ -796,6 +907,9 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
     else unit_L_fast<0>(o, nKbm, ps, n_min);
     return;
   }
+  const uint64_t p2 = (uint64_t)p * p;
+  const bool live = p2 < Vend;
+  const bool slow = p2 > Vs;
   const uint32_t D = slow && live ? (uint32_t)(p2 - Vs) : 0u;
   if (!live) return;
   // Primes above KP/2 mark branch-free: two predicated marks (mark_plane<true>).
@@ -1066,7 +1180,10 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         }
       }
       const uint64_t w0 = seg_word0 + 15ull * blk;  // caller's 32-bit word index
-      if (s == 0 && blk == 0) o[0] |= rg.fix0;
+      if (s == 0 && blk == 0) {
+        o[0] |= (uint32_t)rg.fix;
+        o[1] |= (uint32_t)(rg.fix >> 32);
+      }
       const uint64_t bit0 = 32ull * w0;
       if (bit0 + 480 <= rg.nbits) {  // whole block inside the range (a separate path: no phi copies of o[])
         uint32_t cnt = 0;
@@ -1376,6 +1493,10 @@ static_assert(kBucketCols % 64 == 0, "column scan: whole lanes");
 #define DSE_BK_SPLIT_LOG 28
 #endif
 constexpr uint32_t kBucketSplitLog = DSE_BK_SPLIT_LOG;  // production split: primes <= 2^28 one-level
+// bucketed ranges bucket the primes above 2^kBucketLoLog (<= kWheelMaxPrime;
+// profiles/r05/window_bucket_lo.txt)
+constexpr uint32_t kBucketLoLog = 19;
+static_assert((1ull << kBucketLoLog) <= kWheelMaxPrime && kBucketLoLog >= 17, "bucket threshold");
 constexpr uint32_t kBucketMaxSegs = DSE_BK_SEGS; // segments per pass (LDS counters)
 constexpr uint32_t kCoprime30 = (1u << 1) | (1u << 7) | (1u << 11) | (1u << 13) | (1u << 17) | (1u << 19) |
                                 (1u << 23) | (1u << 29);
@@ -1421,16 +1542,16 @@ __device__ uint32_t wave_upper_bound(const uint32_t* __restrict__ P, uint32_t lo
   return lo + (uint32_t)__popcll(__ballot(lo + lane < hi && le(lo + lane)));
 }
 
-// range[0] = first table index with p > kWheelMaxPrime, range[1] = first with
-// p^2 > vmax, range[2] = first with p > split (clamped to [range[0], range[1]]).
-// One wave.
-__global__ __launch_bounds__(64) void bucket_range_kernel(const void* __restrict__ table, uint64_t vmax,
+// range[0] = first table index with p > lo_p (the pass's bucket threshold),
+// range[1] = first with p^2 > vmax, range[2] = first with p > split (clamped
+// to [range[0], range[1]]). One wave.
+__global__ __launch_bounds__(64) void bucket_range_kernel(const void* __restrict__ table, uint64_t lo_p, uint64_t vmax,
                                                           uint64_t split, uint32_t* __restrict__ range,
                                                           uint32_t* __restrict__ nspill) {
   const TableHeader* th = reinterpret_cast<const TableHeader*>(table);
   const uint32_t np = th->count == 0xFFFFFFFFu ? 0u : th->count;
   const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
-  const uint32_t i_lo = wave_upper_bound(P, 0, np, kWheelMaxPrime, false);
+  const uint32_t i_lo = wave_upper_bound(P, 0, np, lo_p, false);
   const uint32_t i_hi = max(i_lo, wave_upper_bound(P, i_lo, np, vmax, true));
   const uint32_t i_sp = wave_upper_bound(P, i_lo, i_hi, split, false);
   if (threadIdx.x == 0) {
@@ -1447,7 +1568,7 @@ __device__ __forceinline__ uint64_t bucket_first(uint32_t p, const BucketArgs& b
   const uint64_t p2 = (uint64_t)p * p;
   const uint64_t vlo = max(ba.V0 + 1, p2);
   // floor(vlo / p) from a double quotient: vlo < 2^62 rounds by < 2^9 and
-  // p > 2^20, so the estimate is within 1 of the truth; corrected exactly
+  // p > 2^17, so the estimate is within 1 of the truth; corrected exactly
   uint64_t q = (uint64_t)((double)vlo / (double)p);
   int64_t rs = (int64_t)(vlo - q * p);
   while (rs < 0) { rs += p; --q; }
@@ -1974,31 +2095,34 @@ namespace {
     ++n;
   }
   // primes 3..61 inside the range: the wheel drops 3 and 5, the patterns mark 7..61 themselves
-  constexpr uint32_t small[] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61};
+  constexpr uint32_t small[] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61, 67, 71, 73, 79};
+  static_assert(small[sizeof(small) / sizeof(small[0]) - 1] == kQMax && (kQMax - 3) / 2 < 64, "fix covers 3..kQMax");
   for (uint32_t v : small)
-    if (v >= v_start && (v - v_start) / 2 < rs.nbits) w.fix0 |= 1u << ((v - v_start) / 2);
+    if (v >= v_start && (v - v_start) / 2 < rs.nbits) w.fix |= 1ull << ((v - v_start) / 2);
   for (int g = 0; g < kNG; ++g) w.v0g[g] = (uint16_t)(w.V0 % gmod(g));
   return w;
 }
 
 // A launch over the ranges rs[0..n) (1 <= n <= kMaxRanges, each < 2^31
 // segments in all), their segments in order; thresholds: odd primes up to
-// 61, TA, TB1, TB and kWheelMaxPrime (sieved once).
-[[maybe_unused]] WheelArgs make_wheel_args(const RangeSpec* rs, uint32_t n, uint64_t* plane_lut) {
-  static const auto counts = [] {
-    std::array<uint32_t, 5> c{};
-    const uint32_t lim[5] = {kQMax, TA, TB1, TB, (uint32_t)kWheelMaxPrime};
+// 61, TA, TB1, TB and wheel_max (<= kWheelMaxPrime: the primes above it are
+// bucketed or absent).
+[[maybe_unused]] WheelArgs make_wheel_args(const RangeSpec* rs, uint32_t n, uint64_t* plane_lut,
+                                           uint64_t wheel_max = kWheelMaxPrime) {
+  static const std::vector<uint32_t> odd_primes = [] {  // odd primes <= kWheelMaxPrime (sieved once)
     std::vector<uint8_t> comp(kWheelMaxPrime / 2 + 1, 0);  // comp[i]: 2i + 1 composite
     for (uint64_t i = 1; (2 * i + 1) * (2 * i + 1) <= kWheelMaxPrime; ++i)
       if (!comp[i])
         for (uint64_t j = ((2 * i + 1) * (2 * i + 1)) / 2; j <= kWheelMaxPrime / 2; j += 2 * i + 1) comp[j] = 1;
+    std::vector<uint32_t> v;
     for (uint64_t i = 1; 2 * i + 1 <= kWheelMaxPrime; ++i)
-      if (!comp[i])
-        for (int t = 0; t < 5; ++t) c[t] += 2 * i + 1 <= lim[t];
-    return c;
+      if (!comp[i]) v.push_back((uint32_t)(2 * i + 1));
+    return v;
   }();
+  const uint64_t lim[5] = {kQMax, TA, TB1, TB, std::min<uint64_t>(wheel_max, kWheelMaxPrime)};
   WheelArgs wa{};
-  for (int t = 0; t < 5; ++t) wa.nthr[t] = counts[t];
+  for (int t = 0; t < 5; ++t)
+    wa.nthr[t] = (uint32_t)(std::upper_bound(odd_primes.begin(), odd_primes.end(), lim[t]) - odd_primes.begin());
   uint64_t seg = 0, lut = 0;
   for (uint32_t i = 0; i < n; ++i) {
     wa.r[i] = make_wheel_range(rs[i], i ? &lut : plane_lut);
@@ -2196,13 +2320,17 @@ hipError_t launch_bucketed(const void* table, uint64_t g_start, uint64_t nbits, 
   uint64_t max_segs = kBucketMaxSegs;
   if (opts && opts->bucket_pass_segs >= 1 && opts->bucket_pass_segs < max_segs) max_segs = opts->bucket_pass_segs;
   const uint64_t split = 1ull << (opts && opts->bucket_split_log2 ? opts->bucket_split_log2 : kBucketSplitLog);
+  // primes above lo_p are bucketed: below kWheelMaxPrime for a range that is
+  // bucketed anyway (a prime that hits a segment about once is cheaper as a
+  // bucket entry than as 8 plane slots of an L unit; window: 2^19 -2%)
+  const uint64_t lo_p = 1ull << (opts && opts->bucket_lo_log2 ? opts->bucket_lo_log2 : kBucketLoLog);
   const uint32_t cap_div = opts && opts->bucket_cap_div > 1 ? opts->bucket_cap_div : 1;  // test-only: overflow
   const uint32_t k0_div = opts && opts->bucket_k0_div > 1 ? opts->bucket_k0_div : 1;     // test-only: spills
-  const double a0 = (double)kWheelMaxPrime, b0 = std::min((double)split, (double)root);  // band 0: (a0, b0]
+  const double a0 = (double)lo_p, b0 = std::min((double)split, (double)root);  // band 0: (a0, b0]
   for (uint64_t s0 = 0; s0 < total_seg;) {
     uint64_t ns = std::min<uint64_t>(max_segs, total_seg - s0);
     RangeSpec piece{g_start + s0 * kWheelOutBits, kWheelOutBits, nullptr, count};
-    WheelArgs wa = make_wheel_args(&piece, 1, &plane_lut);  // (wa.nthr)
+    WheelArgs wa = make_wheel_args(&piece, 1, &plane_lut, lo_p);  // (wa.nthr)
     const uint32_t k0_full = bucket_k0(wa.nthr[4], a0, b0);
     while (ns > 1 && (bucket_cap(ns * kWheelSpan, (double)split, (double)root) > kBucketMaxEntries ||
                       4ull * ns * kBucketGrid * k0_full > kBucketMaxRegionBytes))
@@ -2211,7 +2339,7 @@ hipError_t launch_bucketed(const void* table, uint64_t g_start, uint64_t nbits, 
     const uint64_t nb = std::min<uint64_t>(nbits - s0 * kWheelOutBits, ns * kWheelOutBits);
     const uint64_t vmax_p = 3 + 2 * (g0 + nb - 1);
     piece = {g0, nb, out ? out + s0 * (kWheelOutBits / 32) : nullptr, count};
-    wa = make_wheel_args(&piece, 1, &plane_lut);
+    wa = make_wheel_args(&piece, 1, &plane_lut, lo_p);
     BucketArgs ba{};
     ba.V0 = wa.r[0].V0;
     ba.span = ns * kWheelSpan;
@@ -2220,7 +2348,7 @@ hipError_t launch_bucketed(const void* table, uint64_t g_start, uint64_t nbits, 
     ba.vmax = vmax_p;
     ba.split = split;
     const uint64_t root_p = isqrt64(vmax_p);
-    const bool band0 = split > kWheelMaxPrime, band1 = split < root_p;
+    const bool band0 = split > lo_p, band1 = split < root_p;
     // band 1: rigorous entry capacity (its keys, then its sorted entries);
     // band 0: regions of k0 slots per (segment, fill workgroup), the spill
     // list's capacity a rigorous bound on the band's hits
@@ -2260,7 +2388,8 @@ hipError_t launch_bucketed(const void* table, uint64_t g_start, uint64_t nbits, 
     bz.spill_cap = spill_cap;
     bz.flag = scratch->flag;
     bz.count = count;
-    hipLaunchKernelGGL(bucket_range_kernel, dim3(1), dim3(64), 0, stream, table, vmax_p, ba.split, range, bz.nspill);
+    hipLaunchKernelGGL(bucket_range_kernel, dim3(1), dim3(64), 0, stream, table, lo_p, vmax_p, ba.split, range,
+                       bz.nspill);
     hipLaunchKernelGGL(bucket_count_kernel, dim3(kBucketGrid1), dim3(kBucketThreads), 4 * (uint32_t)ns, stream, table,
                        ba, range, cols);
     hipLaunchKernelGGL(bucket_colscan_kernel, dim3((uint32_t)((ns + 3) / 4)), dim3(256), 0, stream, cols,

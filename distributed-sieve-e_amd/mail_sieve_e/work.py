@@ -67,7 +67,8 @@ def marks_for_range(g_start: int, nbits: int) -> int:
 
 R30 = (1, 7, 11, 13, 17, 19, 23, 29)
 WHEEL_OUT_BITS = 15 * 2**17  # odd candidates per wheel-kernel segment (csrc/dse_internal.h kWheelOutBits)
-WHEEL_PATTERN_MAX = 61  # the wheel kernel ORs register patterns for 7..61 (no LDS marks)
+WHEEL_PATTERN_MAX = 79  # the wheel kernel's init lays down the patterns of 7..79 (no LDS marks; csrc kQMax)
+WHEEL_PATTERN_GROUPS = 9  # in 9 groups of 1-3 primes (csrc kNG)
 
 
 def _coprime30_upto(x: np.ndarray) -> np.ndarray:
@@ -78,8 +79,8 @@ def _coprime30_upto(x: np.ndarray) -> np.ndarray:
 
 def wheel_marks_for_range(g_start: int, nbits: int) -> int:
     """LDS marks the mod-30 wheel kernel issues for the odd-index range:
-    multiples p*m >= p^2 with gcd(m, 30) = 1 of every prime 61 < p <= sqrt(vmax)
-    (multiples of 3 and 5 are not stored, primes 7..61 are register patterns)."""
+    multiples p*m >= p^2 with gcd(m, 30) = 1 of every prime 79 < p <= sqrt(vmax)
+    (multiples of 3 and 5 are not stored, primes 7..79 are init patterns)."""
     if nbits <= 0:
         return 0
     va = 3 + 2 * g_start

@@ -196,6 +196,9 @@ int32_t dse_device_status(dse_ctx *ctx);
  *   "scratch_poison" = 1: fill the bucket scratch with 0xFF bytes before
  *   every bucketed pass (stale contents: results unchanged, and an overflowed
  *   pass still reads only what it wrote); 0 = default.
+ *   "bucket_lo_log2" = k in 17..20: a range that needs the bucketed pass
+ *   (sqrt of its largest value above 2^20) buckets every prime above 2^k
+ *   instead of the production threshold; 0 = default.
  *   "rccl_single" = 1: give a one-device context (dse_init(1) or
  *   dse_init_device) a 1-rank RCCL communicator (ncclCommInitAll), so
  *   dse_sieve_all / dse_sieve_window issue the same grouped ncclBroadcast of

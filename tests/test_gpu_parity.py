@@ -602,3 +602,54 @@ def test_pooled_chunks_vs_oracle(oracle, geometry):
                 assert np.array_equal(c.copy_chunk_mask(N, P, k + 1), m_ref), (geometry, N, P, k)
             t_ref = oracle.fast_sieve_range(tail_g, tail_n, want_mask=False)[1] if tail_n else 0
             assert pi_full - pi_ref == t_ref, (geometry, N, P)
+
+
+@pytest.mark.parametrize("lo", [17, 18, 20])
+def test_bucket_lo_threshold_mask(oracle, lo):
+    """The bucket threshold of bucketed ranges (production 2^19; test-only
+    option bucket_lo_log2): the primes in (2^lo, 2^20] move between the wheel
+    kernel's L units and the band-0 fill; a 1e13 range (base primes up to
+    3.2e6) and a 1e16 range (up to 1e8), each in one pass and in passes of 3
+    segments, bit-exact against the oracle."""
+    from mail_sieve_e import sieve as S
+    for g0, nb in (((10**13 + 1 - 3) // 2, 5 * 10**7), (10**16 // 2 + 12345, 20 * 983040 + 777)):
+        m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
+        with S.Context(num_gpus=1) as c:
+            c.debug_set_option("bucket_lo_log2", lo)
+            m, cnt = c.sieve_odd_range(g0, nb)
+            assert cnt == c_ref and np.array_equal(m, m_ref), (lo, g0)
+            c.debug_set_option("bucket_pass_segments", 3)
+            m, cnt = c.sieve_odd_range(g0, nb)
+            assert cnt == c_ref and np.array_equal(m, m_ref), (lo, g0, 3)
+    with S.Context(num_gpus=1) as c:
+        from mail_sieve_e import _dse
+        for bad in (1, 16, 21):
+            with pytest.raises(_dse.DseError):
+                c.debug_set_option("bucket_lo_log2", bad)
+
+
+def test_pooled_and_bucketed_chunks_in_one_call(ctx):
+    """One dse_sieve_all call whose chunks take both paths of
+    launch_sieve_ranges: N = 1.2e12, P = 8 on one device, chunks
+    1-7 (the square root of their largest value below 2^20) pooled into one
+    persistent launch, chunk 8 through the bucketed pass, issued inline before
+    the pooled launch on the same stream with the same count slots. Every
+    chunk's count, and the masks of chunk 7 (pooled, last of the launch) and
+    chunk 8 (bucketed), equal the single-range path (dse_sieve_odd_range, one
+    range per call); pi_ref + the tail equals the one-range count of [3, N]."""
+    N, P = 12 * 10**11, 8
+    cs = (N - 1) // 2 // P
+    counts, pi_ref, pi_full = ctx.sieve_all(N, P)
+    import math
+    assert math.isqrt(3 + 2 * (7 * cs - 1)) <= 2**20 < math.isqrt(3 + 2 * (8 * cs - 1))
+    for k in (7, 8):
+        m, c = ctx.sieve_odd_range((k - 1) * cs, cs)
+        assert int(counts[k - 1]) == c, k
+        assert np.array_equal(ctx.copy_chunk_mask(N, P, k), m), k
+        del m
+    for k in range(1, 7):
+        _, c = ctx.sieve_odd_range((k - 1) * cs, cs, want_mask=False)
+        assert int(counts[k - 1]) == c, k
+    _, whole = ctx.sieve_odd_range(0, (N - 1) // 2, want_mask=False)
+    assert pi_full == 1 + whole
+    assert pi_ref == 1 + sum(int(x) for x in counts)
