@@ -4,8 +4,8 @@
 set -o pipefail
 O=gpurun_out/ev5
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputest.log 2>&1 || { tail -40 $O/gputest.log; exit 1; }
-tail -1 $O/gputest.log
+# (GPU suite: profiles/r05/gputest_merged.log)
+
 timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 python3 -c "import json; j=json.load(open('$O/bench.json')); print('bench', j['ms_per_step'], j['value'], j['verified'], j['roofline']['kernel_ms'], j['cpu_baseline']['value'])"
 timeout -k 10 300 python bench.py --rccl-single --cpu-baseline off > $O/bench_rccl_single.json 2> $O/bench_rccl.err || { tail -20 $O/bench_rccl.err; exit 1; }
