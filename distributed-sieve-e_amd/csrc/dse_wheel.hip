@@ -160,6 +160,8 @@ constexpr InitTables make_init_tables() {
 }
 __device__ const InitTables g_init_tables = make_init_tables();
 
+constexpr uint32_t kLPieces = 16;  // pieces of a range with their own large-prime bound
+
 // One odd-index range of a launch: its segments are [seg0, seg0 + its
 // segment count) of the launch's list (WheelArgs::nseg in all).
 struct WheelRange {
@@ -174,6 +176,11 @@ struct WheelRange {
   uint64_t fix;        // output words 0, 1: bits of the primes 3..kQMax inside the range
   uint32_t seg0;       // first segment of the range in the launch
   uint16_t v0g[kNG];   // V0 mod M_G (init tables)
+  // Large units past the live primes of a segment only load operands to skip
+  // them: segment s of the range needs table indices below
+  // lcap[min(s >> lsh, kLPieces - 1)] (>= the odd primes with p^2 < its end)
+  uint32_t lsh;
+  uint32_t lcap[kLPieces];
 };
 // Ranges per launch: several chunks of one device (dse_sieve_all with P >
 // devices, and the dropped tail) go to one persistent launch, so no chunk's
@@ -198,6 +205,7 @@ struct WheelArgs {
   uint64_t bk_spill_cap;               //   (at most this many stored)
   uint32_t bk_k0;              // band-0 region capacity (0: no band 0 in the pass)
 };
+static_assert(sizeof(WheelArgs) <= 4096, "kernel arguments");
 
 // 32-bit LDS byte address of a __shared__ pointer.
 __device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
@@ -1034,8 +1042,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
   const uint32_t nB2 = (i_mid1 - i_midB2 + 7) / 8;
   const uint32_t i_big = s_thr[4];             // L units end here
   constexpr uint32_t kLU = 128;                // primes per L unit
-  const uint32_t nL = (i_big - i_mid1 + kLU - 1) / kLU;
-  const uint32_t n1 = nA + nB1 + nB2, n2 = nL;
+  const uint32_t n1 = nA + nB1 + nB2;
 
   const uint32_t nseg = wa.nseg;
   const uint32_t grid = gridDim.x;
@@ -1274,6 +1281,9 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     // atomic for unit j+2 is issued when unit j starts and read when it ends
     // (by then this wave's marks of unit j have drained), and a large unit's
     // operands are loaded while the unit before it runs.
+    // large units of this segment: up to its piece's bound (WheelRange::lcap)
+    const uint32_t i_live = max(i_mid1, min(i_big, rg.lcap[min((uint32_t)(s >> rg.lsh), kLPieces - 1)]));
+    const uint32_t n2 = (i_live - i_mid1 + kLU - 1) / kLU;
     const uint32_t n_int = min(n1, n2), n_all = n1 + n2;
     // The claim is an asm ds_add_rtn: written as a C++ atomic, the AMDGPU
     // atomic optimizer aggregates it over the wave and waits for its return
@@ -2147,9 +2157,22 @@ constexpr uint64_t kNtStoreMinRoot = DSE_NT_MIN_ROOT;  // base primes above this
     wa.nthr[t] = (uint32_t)(std::upper_bound(odd_primes.begin(), odd_primes.end(), lim[t]) - odd_primes.begin());
   uint64_t seg = 0, lut = 0;
   for (uint32_t i = 0; i < n; ++i) {
-    wa.r[i] = make_wheel_range(rs[i], i ? &lut : plane_lut);
-    wa.r[i].seg0 = (uint32_t)seg;
-    seg += (rs[i].nbits + kWheelOutBits - 1) / kWheelOutBits;
+    WheelRange& r = wa.r[i];
+    r = make_wheel_range(rs[i], i ? &lut : plane_lut);
+    r.seg0 = (uint32_t)seg;
+    const uint64_t nseg_r = (rs[i].nbits + kWheelOutBits - 1) / kWheelOutBits;
+    seg += nseg_r;
+    // piece j = segments [j << lsh, (j + 1) << lsh): the odd primes with p^2
+    // below the end of its last segment (the kernel's live test is p^2 < Vend)
+    r.lsh = 0;
+    while (nseg_r > 0 && ((nseg_r - 1) >> r.lsh) >= kLPieces) ++r.lsh;
+    for (uint32_t j = 0; j < kLPieces; ++j) {
+      const uint64_t last = nseg_r == 0 ? 0 : std::min<uint64_t>(((uint64_t)(j + 1) << r.lsh) - 1, nseg_r - 1);
+      const uint64_t vend = r.V0 + (last + 1) * (uint64_t)kWheelSpan;
+      r.lcap[j] = (uint32_t)(std::upper_bound(odd_primes.begin(), odd_primes.end(), isqrt64(vend - 1)) -
+                             odd_primes.begin());
+      if (r.lcap[j] == odd_primes.size()) r.lcap[j] = ~0u;  // past kWheelMaxPrime: no bound
+    }
   }
   wa.nranges = n;
   wa.nseg = (uint32_t)seg;

@@ -12,7 +12,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "distributed-sieve-e_amd")]
 import torch  # noqa: E402
-from mail_sieve_e import sieve as S  # noqa: E402
+from mail_sieve_e import _dse, sieve as S  # noqa: E402
+
+if os.environ.get("DSE_LIB"):  # A/B another build of the library
+    _dse.LIB_PATH = os.environ["DSE_LIB"]
 
 
 def main():
