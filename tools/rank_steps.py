@@ -3,7 +3,7 @@ the base table build plus the sieve of every spread-work chunk k of P, each
 timed with HIP events on the launch stream (median of 5). The max over chunks
 is the multi-GPU critical path without the collectives.
 
-  python tools/rank_steps.py [N] [P]
+  python tools/rank_steps.py [N] [P]     (DSE_OPTS=name=value,... sets test-only options)
 """
 import os
 import statistics
@@ -23,6 +23,9 @@ def main():
     P = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     dev = torch.device("cuda", 0)
     ctx = S.Context(device=0)
+    for kv in filter(None, os.environ.get("DSE_OPTS", "").split(",")):  # test-only options, name=value
+        k, v = kv.split("=")
+        ctx.debug_set_option(k, int(v))
     cs = (N - 1) // 2 // P
     tail_n = (N - 1) // 2 - P * cs
     limit = S.base_limit_for_range(0, P * cs + tail_n)
