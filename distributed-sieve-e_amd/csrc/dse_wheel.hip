@@ -191,7 +191,6 @@ constexpr uint32_t kMaxRanges = 9;
 struct WheelArgs {
   WheelRange r[kMaxRanges];
   uint32_t nranges;    // 1..kMaxRanges (1 with bucketed primes)
-  uint32_t nt_store;   // 1: mask stores non-temporal (large operand tables, make_wheel_args)
   uint32_t nseg;       // segments of all ranges
   uint32_t nthr[5];    // odd primes <= 61, TA, TB1, TB, kWheelMaxPrime (table indices of the unit lists)
   // Bucketed hits of the primes > kWheelMaxPrime (bk_start null: none), as
@@ -909,7 +908,9 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
   // ascend (lanes past the table end hold 0x7FFFFFFF), so pmax decides, on
   // the scalar unit (a per-lane 64-bit p^2 and two compares: 1e12 +1.4%)
   const bool none = (uint64_t)pmax * pmax > Vs;
-  const uint32_t n_min = (none || pmax >= KP) ? 0u : div_small(KP - pmax, pmax, fast_rcp((float)pmax));
+  // every plane start kk is below p <= pmax (plane_start), so each lane has at
+  // least floor(KP / pmax) hits per plane: kk + (n - 1) p <= p - 1 + KP - p
+  const uint32_t n_min = (none || pmax >= KP) ? 0u : div_small(KP, pmax, fast_rcp((float)pmax));
   if (!none) {  // every lane live and past p^2: branch-free bodies
     if (pmin > KP) unit_L_fast<2>(o, nKbm, ps, 0);
     else if (pmin > KP / 2) unit_L_fast<1>(o, nKbm, ps, 0);
@@ -1199,17 +1200,8 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         for (int w = 0; w < 15; ++w) cnt += __popc(o[w]);
         my_count += cnt;
         if (out) {
-          if (wa.nt_store) {
-            // an opaque copy of the pointer keeps the compiler from merging
-            // both branches' stores into one (which drops the hint)
-            __attribute__((address_space(1))) uint32_t* nto = (__attribute__((address_space(1))) uint32_t*)out;
-            asm volatile("" : "+v"(nto));
 #pragma unroll
-            for (int w = 0; w < 15; ++w) __builtin_nontemporal_store(o[w], nto + w0 + w);
-          } else {
-#pragma unroll
-            for (int w = 0; w < 15; ++w) out[w0 + w] = o[w];
-          }
+          for (int w = 0; w < 15; ++w) out[w0 + w] = o[w];
         }
       } else {  // range end (last segment only): mask, count, store what is inside the caller's words
         const uint32_t rem = bit0 >= rg.nbits ? 0u : (uint32_t)(rg.nbits - bit0);  // < 480 valid bits
@@ -2130,11 +2122,6 @@ namespace {
   return r;
 }
 
-#ifndef DSE_NT_MIN_ROOT
-#define DSE_NT_MIN_ROOT 400000
-#endif
-constexpr uint64_t kNtStoreMinRoot = DSE_NT_MIN_ROOT;  // base primes above this: non-temporal mask stores
-
 // A launch over the ranges rs[0..n) (1 <= n <= kMaxRanges, each < 2^31
 // segments in all), their segments in order; thresholds: odd primes up to
 // 61, TA, TB1, TB and wheel_max (<= kWheelMaxPrime: the primes above it are
@@ -2176,14 +2163,9 @@ constexpr uint64_t kNtStoreMinRoot = DSE_NT_MIN_ROOT;  // base primes above this
   }
   wa.nranges = n;
   wa.nseg = (uint32_t)seg;
-  // Non-temporal mask stores once the large units' operand rows (re-read by
-  // every segment) compete with the mask stream for the L2: streaming stores
-  // keep the rows resident (N=1e12 -5.1%, 4e11 -4.5%); with a small table
-  // they cost a little (1e11 +0.6%), window neutral.
-  // profiles/r05/ab_nt_store_policy.txt, window_nt_store.txt
-  uint64_t root = 0;
-  for (uint32_t i = 0; i < n; ++i) root = std::max(root, isqrt64(3 + 2 * (rs[i].g_start + rs[i].nbits - 1)));
-  wa.nt_store = std::min(root, wheel_max) > kNtStoreMinRoot ? 1u : 0u;
+  // (Non-temporal mask stores paid 5% at 1e12 only while segments claimed the
+  // dead large units past their live primes; with lcap they do not:
+  // profiles/r05/ab_nt_store_policy.txt, ab_nmin_and_nt_recheck.txt)
   return wa;
 }
 

@@ -1,0 +1,10 @@
+# MODE-0 unconditional marks floor(KP / pmax) (prod) against HEAD (lc); store policy re-check (nt0/ntinf built on lc)
+set -o pipefail
+O=gpurun_out/r5nmin
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gputest.log 2>&1 || { tail -30 $O/gputest.log; exit 1; }
+tail -1 $O/gputest.log
+OUT=$O N=1e11 ROUNDS=3 TMO=500 bash tools/gpu/ab.sh prod lc > /dev/null || exit 1
+OUT=$O N=1e12 ROUNDS=2 TMO=600 bash tools/gpu/ab.sh prod lc nt0 ntinf > /dev/null || exit 1
+OUT=$O N=4e11 ROUNDS=2 TMO=500 bash tools/gpu/ab.sh lc nt0 ntinf > /dev/null || exit 1
+cat $O/ab_*.txt
