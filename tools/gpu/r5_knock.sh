@@ -1,0 +1,7 @@
+# per-class knockouts of the current kernel at 1e11: PMC table + kernel time of each build
+set -o pipefail
+O=gpurun_out/r5ko
+mkdir -p $O
+OUT=$O N=1e11 bash tools/gpu/knockout_pmc.sh 0 1 2 4 8 16 32 || exit 1
+OUT=$O N=1e11 ROUNDS=2 TMO=500 bash tools/gpu/ab.sh ko0 ko1 ko2 ko4 ko8 ko16 ko32 > /dev/null || exit 1
+cat $O/ab_1e11.txt
