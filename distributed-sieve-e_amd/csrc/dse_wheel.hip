@@ -321,6 +321,43 @@ __device__ __forceinline__ void mark_tail(uint32_t pb4, uint32_t k, uint32_t p, 
       : "memory", "vcc");
 }
 
+// The rest of a walk known to be at most T (1 or 2) steps: T predicated marks,
+// no loop (mark_tail's loop costs 2 more VALU and 2-3 branches for 1-2
+// steps). The second mark's lanes are a subset of the first's, so exec is
+// narrowed twice and restored once, all inside the block.
+template <int T>
+__device__ __forceinline__ void mark_tail_n(uint32_t pb4, uint32_t k, uint32_t p, uint32_t one) {
+  uint64_t sv;
+  uint32_t a, b;
+  if (T == 1)
+    asm volatile(
+        "s_mov_b64 %3, exec\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %5, %2\n\t"
+        "v_and_or_b32 %0, %2, %6, %7\n\t"
+        "v_lshlrev_b32 %1, %2, %8\n\t"
+        "ds_or_b32 %0, %1\n\t"
+        "s_mov_b64 exec, %3"
+        : "=&v"(a), "=&v"(b), "+v"(k), "=&s"(sv)
+        : "v"(p), "s"(KP), "s"(kBlockMask), "v"(pb4), "v"(one)
+        : "memory", "vcc");
+  else
+    asm volatile(
+        "s_mov_b64 %3, exec\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %5, %2\n\t"
+        "v_and_or_b32 %0, %2, %6, %7\n\t"
+        "v_lshlrev_b32 %1, %2, %8\n\t"
+        "v_add_u32 %2, %2, %4\n\t"
+        "ds_or_b32 %0, %1\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %5, %2\n\t"
+        "v_and_or_b32 %0, %2, %6, %7\n\t"
+        "v_lshlrev_b32 %1, %2, %8\n\t"
+        "ds_or_b32 %0, %1\n\t"
+        "s_mov_b64 exec, %3"
+        : "=&v"(a), "=&v"(b), "+v"(k), "=&s"(sv)
+        : "v"(p), "s"(KP), "s"(kBlockMask), "v"(pb4), "v"(one)
+        : "memory", "vcc");
+}
+
 // ds_or_b32 at a precomputed LDS byte address.
 __device__ __forceinline__ void mark_at(uint32_t a, uint32_t bit) {
   asm volatile("ds_or_b32 %0, %1" : : "v"(a), "v"(bit) : "memory");
@@ -852,7 +889,9 @@ __device__ __forceinline__ void start_marks4(const uint32_t* a, const uint32_t* 
         : "memory", "vcc");
 }
 
-template <int MODE>
+// MODE 0 with TT = 1 or 2: at most TT hits per plane after the n_min run
+// (mark_tail_n); TT = 0: the loop.
+template <int MODE, int TT = 0>
 __device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, const PlaneSteps& ps,
                                             uint32_t n_min) {
   const uint32_t p = o.p;
@@ -866,7 +905,8 @@ __device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, co
     uint32_t kk = plane_start(o.a[q], nKbm, ps.ne[q], p);
     const uint32_t pb4 = ps.pb[q];
     kk = mark_run(pb4, kk, p, n_min, ps.one);
-    mark_tail(pb4, kk, p, ps.one);
+    if (TT == 0) mark_tail(pb4, kk, p, ps.one);
+    else mark_tail_n<TT>(pb4, kk, p, ps.one);
   }
 }
 
@@ -914,7 +954,15 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
   if (!none) {  // every lane live and past p^2: branch-free bodies
     if (pmin > KP) unit_L_fast<2>(o, nKbm, ps, 0);
     else if (pmin > KP / 2) unit_L_fast<1>(o, nKbm, ps, 0);
-    else unit_L_fast<0>(o, nKbm, ps, n_min);
+    else {
+      // a lane has at most ceil(KP / p) <= ceil(KP / pmin) hits per plane, so
+      // at most n_tail after the run
+      const uint32_t n_tail =
+          (uint32_t)__builtin_amdgcn_readfirstlane(div_ceil_small(KP, pmin, fast_rcp((float)pmin))) - n_min;
+      if (pmax < KP && n_tail == 1) unit_L_fast<0, 1>(o, nKbm, ps, n_min);
+      else if (pmax < KP && n_tail == 2) unit_L_fast<0, 2>(o, nKbm, ps, n_min);
+      else unit_L_fast<0>(o, nKbm, ps, n_min);
+    }
     return;
   }
   const uint64_t p2 = (uint64_t)p * p;
