@@ -282,6 +282,7 @@ __device__ __forceinline__ void mark_k_step4(uint32_t pb4, uint32_t& k, uint32_t
       : "memory");
 }
 
+
 // n unconditional marks k, k + p, ... (by 4: three SALU of loop control per
 // mark otherwise); returns the index after the run.
 __device__ __forceinline__ uint32_t mark_run(uint32_t pb4, uint32_t k, uint32_t p, uint32_t n, uint32_t one) {
@@ -775,9 +776,12 @@ __device__ __forceinline__ uint32_t plane_start(uint32_t a, uint32_t nKbm, uint3
 // Branch-free body of an L unit whose 64 primes are all live and past p^2
 // (the common case): the mark count per plane is decided once per unit.
 // MODE 2: pmin > KP, one predicated mark per plane; MODE 1: pmin > KP/2, two;
-// MODE 0: n_min unconditional marks per plane and a short loop for the rest.
+// MODE 3: MODE 1 with pmax < KP, whose first mark every lane has (kk < p < KP),
+// so only the second is predicated; MODE 0: n_min unconditional marks per
+// plane and a short loop for the rest.
 // MODE 1/2: four planes per block, each a plane start (a - Kb - e) mod p and
-// its NM = 1 or 2 predicated marks kk, kk + p; a plane's second mark's lanes
+// its NM = 1 or 2 predicated marks kk, kk + p (NM = 3: two, the first
+// unconditional); a plane's second mark's lanes
 // are a subset of its first's, so exec is narrowed twice and restored once
 // per plane, from the copy the block saved on entry. Every exec write is
 // inside the block, so no code the compiler places between blocks can run
@@ -828,7 +832,7 @@ __device__ __forceinline__ void start_marks4(const uint32_t* a, const uint32_t* 
         : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(ne[0]), "v"(ne[1]), "v"(ne[2]), "v"(ne[3]), "v"(pb[0]),
           "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(nKbm), "v"(p), "s"(KP), "s"(kBlockMask), "v"(one)
         : "memory", "vcc");
-  else
+  else if (NM == 2)
     asm volatile(
         "s_mov_b64 %3, exec\n\t"
         "v_add3_u32 %0, %4, %16, %8\n\t"
@@ -887,6 +891,61 @@ __device__ __forceinline__ void start_marks4(const uint32_t* a, const uint32_t* 
         : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(ne[0]), "v"(ne[1]), "v"(ne[2]), "v"(ne[3]), "v"(pb[0]),
           "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(nKbm), "v"(p), "s"(KP), "s"(kBlockMask), "v"(one)
         : "memory", "vcc");
+  else  // NM == 3: two marks, the first unconditional (every lane has kk < p <= pmax < KP)
+    asm volatile(
+        "s_mov_b64 %3, exec\n\t"
+        "v_add3_u32 %0, %4, %16, %8\n\t"
+        "v_add_u32 %1, %0, %17\n\t"
+        "v_min_u32 %0, %0, %1\n\t"
+        "v_and_or_b32 %1, %0, %19, %12\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "v_add_u32 %0, %0, %17\n\t"
+        "v_and_or_b32 %1, %0, %19, %12\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %3\n\t"
+        "v_add3_u32 %0, %5, %16, %9\n\t"
+        "v_add_u32 %1, %0, %17\n\t"
+        "v_min_u32 %0, %0, %1\n\t"
+        "v_and_or_b32 %1, %0, %19, %13\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "v_add_u32 %0, %0, %17\n\t"
+        "v_and_or_b32 %1, %0, %19, %13\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %3\n\t"
+        "v_add3_u32 %0, %6, %16, %10\n\t"
+        "v_add_u32 %1, %0, %17\n\t"
+        "v_min_u32 %0, %0, %1\n\t"
+        "v_and_or_b32 %1, %0, %19, %14\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "v_add_u32 %0, %0, %17\n\t"
+        "v_and_or_b32 %1, %0, %19, %14\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %3\n\t"
+        "v_add3_u32 %0, %7, %16, %11\n\t"
+        "v_add_u32 %1, %0, %17\n\t"
+        "v_min_u32 %0, %0, %1\n\t"
+        "v_and_or_b32 %1, %0, %19, %15\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "v_add_u32 %0, %0, %17\n\t"
+        "v_and_or_b32 %1, %0, %19, %15\n\t"
+        "v_lshlrev_b32 %2, %0, %20\n\t"
+        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
+        "ds_or_b32 %1, %2\n\t"
+        "s_mov_b64 exec, %3"
+        : "=&v"(t), "=&v"(u), "=&v"(b), "=&s"(sv)
+        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(ne[0]), "v"(ne[1]), "v"(ne[2]), "v"(ne[3]), "v"(pb[0]),
+          "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(nKbm), "v"(p), "s"(KP), "s"(kBlockMask), "v"(one)
+        : "memory", "vcc");
 }
 
 // MODE 0 with TT = 1 or 2: at most TT hits per plane after the n_min run
@@ -896,8 +955,9 @@ __device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, co
                                             uint32_t n_min) {
   const uint32_t p = o.p;
   if (MODE != 0) {
-    start_marks4<MODE == 1 ? 2 : 1>(o.a, ps.ne, ps.pb, nKbm, p, ps.one);
-    start_marks4<MODE == 1 ? 2 : 1>(o.a + 4, ps.ne + 4, ps.pb + 4, nKbm, p, ps.one);
+    constexpr int NM = MODE == 2 ? 1 : MODE == 1 ? 2 : 3;  // MODE 3: MODE 1 with pmax < KP
+    start_marks4<NM>(o.a, ps.ne, ps.pb, nKbm, p, ps.one);
+    start_marks4<NM>(o.a + 4, ps.ne + 4, ps.pb + 4, nKbm, p, ps.one);
     return;
   }
 #pragma unroll
@@ -953,6 +1013,7 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
   const uint32_t n_min = (none || pmax >= KP) ? 0u : div_small(KP, pmax, fast_rcp((float)pmax));
   if (!none) {  // every lane live and past p^2: branch-free bodies
     if (pmin > KP) unit_L_fast<2>(o, nKbm, ps, 0);
+    else if (pmin > KP / 2 && pmax < KP) unit_L_fast<3>(o, nKbm, ps, 0);
     else if (pmin > KP / 2) unit_L_fast<1>(o, nKbm, ps, 0);
     else {
       // a lane has at most ceil(KP / p) <= ceil(KP / pmin) hits per plane, so
