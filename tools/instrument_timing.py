@@ -38,7 +38,8 @@ def main(root):
     p = os.path.join(out, "dse_wheel.hip")
     s = open(p).read()
     s = sub(s, "namespace dse {\nnamespace {\n",
-            "namespace dse {\nnamespace {\n__device__ unsigned long long g_timing[16];\n")
+            "namespace dse {\nnamespace {\n__device__ unsigned long long g_timing[16];\n"
+            "__device__ unsigned long long g_timing_w[16 * 5];  // per wave id: the 5 phases\n")
     s = sub(s, "  const uint32_t tid = threadIdx.x, lane_id = tid & 63, wave = tid >> 6;\n",
             "  const uint32_t tid = threadIdx.x, lane_id = tid & 63, wave = tid >> 6;\n"
             "  uint64_t t_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, t_prev = 0;\n"
@@ -69,7 +70,8 @@ def main(root):
             "    if (t + 1 < T) init_segment(lds.img, s + grid);\n    DSE_TSTAMP(3);\n    if (tid == 0) {\n")
     s = sub(s, "    __syncthreads();\n  }\n\n  if (tid < wa.nranges && lds.rcnt[tid])",
             "    __syncthreads();\n    DSE_TSTAMP(4);\n  }\n"
-            "  if (lane_id == 0)\n    for (int i = 0; i < 10; ++i) atomicAdd(&g_timing[i], (unsigned long long)t_acc[i]);\n\n"
+            "  if (lane_id == 0)\n    for (int i = 0; i < 10; ++i) atomicAdd(&g_timing[i], (unsigned long long)t_acc[i]);\n"
+            "  if (lane_id == 0)\n    for (int i = 0; i < 5; ++i) atomicAdd(&g_timing_w[wave * 5 + i], (unsigned long long)t_acc[i]);\n\n"
             "  if (tid < wa.nranges && lds.rcnt[tid])")
     s = sub(s, "}  // namespace dse\n", """#if DSE_WHEEL_PLAIN_TU
 int timing_take_plain(unsigned long long* acc) {
@@ -80,15 +82,20 @@ int timing_take_plain(unsigned long long* acc);
 int timing_take_half(unsigned long long* acc);
 int timing_take_main(unsigned long long* acc) {
 #endif
-  unsigned long long t[16];
+  unsigned long long t[16], tw[80];
   if (hipMemcpyFromSymbol(t, HIP_SYMBOL(g_timing), sizeof(t)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(tw, HIP_SYMBOL(g_timing_w), sizeof(tw)) != hipSuccess) return -1;
   for (int i = 0; i < 16; ++i) acc[i] += t[i];
-  const unsigned long long z[16] = {};
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_timing), z, sizeof(z)) == hipSuccess ? 0 : -1;
+  for (int i = 0; i < 80; ++i) acc[16 + i] += tw[i];
+  const unsigned long long z[80] = {};
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_timing_w), z, sizeof(tw)) != hipSuccess) return -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_timing), z, sizeof(t)) == hipSuccess ? 0 : -1;
 }
 #if DSE_WHEEL_MAIN_TU
+// out[0..16): phase and unit sums over all waves; out[16 + 5 w + i]: phase i
+// (mark, mark barrier, expand, init, segment barrier) of the waves with id w
 extern "C" int dse_debug_timing(unsigned long long* out) {
-  for (int i = 0; i < 16; ++i) out[i] = 0;
+  for (int i = 0; i < 96; ++i) out[i] = 0;
   return (timing_take_main(out) || timing_take_plain(out) || timing_take_half(out)) ? -1 : 0;
 }
 #endif

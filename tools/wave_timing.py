@@ -21,7 +21,7 @@ CLK = 2.4e9
 
 
 def take():
-    buf = (ctypes.c_ulonglong * 16)()
+    buf = (ctypes.c_ulonglong * 96)()
     assert _dse.lib().dse_debug_timing(buf) == 0
     return list(buf)
 
@@ -40,6 +40,11 @@ def report(label, fn, waves):
     rest = t[0] - sum(t[5:10])
     print(f"{'  unit loop rest':24s} {rest / waves / CLK * 1e3:8.3f} ms per wave")
     print(f"{'sum':24s} {total / waves / CLK * 1e3:8.3f} ms per wave", flush=True)
+    # per wave id (256 waves each): mark, mark barrier, expand, init, segment barrier
+    print("wave id   mark  mark-wait  expand   init  seg-wait  (ms per wave)")
+    for w in range(16):
+        r = [t[16 + 5 * w + i] / (waves // 16) / CLK * 1e3 for i in range(5)]
+        print(f"{w:7d} " + " ".join(f"{x:7.3f}" for x in r), flush=True)
 
 
 def main():
