@@ -347,6 +347,30 @@ def test_table_from_broadcast_primes(ctx, limit):
     assert outs[0][1] == outs[1][1] > 0 and torch.equal(outs[0][0], outs[1][0])
 
 
+@pytest.mark.parametrize("g0,nseg", [(0, 64), (12345, 37), (10**9 + 7, 20), (4 * 10**10, 9)])
+def test_table_beyond_range_root(ctx, oracle, g0, nseg):
+    """A table built for N=1e12 (primes to 1e6) over ranges whose own roots
+    are far smaller: each sixteenth of a range claims large units only up to
+    its last prime with p^2 below its end (WheelRange::lcap), so the bound
+    moves from piece to piece (64 segments from 0: pieces of 4 segments).
+    Masks and counts against the oracle."""
+    import torch
+    dev = torch.device("cuda", 0)
+    limit = 1_000_003
+    from mail_sieve_e import sieve as S
+    tbytes = S.base_table_bytes(limit)
+    table = torch.empty(tbytes, dtype=torch.uint8, device=dev)
+    ctx.base_primes_dev_async(limit, table.data_ptr(), tbytes, 0)
+    nb = nseg * 1966080 - 4321
+    mask = torch.zeros((nb + 63) // 64, dtype=torch.int64, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    ctx.sieve_range_dev_async(table.data_ptr(), g0, nb, mask.data_ptr(), cnt.data_ptr(), 0)
+    torch.cuda.synchronize()
+    m_ref, c_ref = oracle.fast_sieve_range(g0, nb)
+    assert int(cnt.item()) == c_ref
+    assert np.array_equal(mask.cpu().numpy().view(np.uint64), m_ref.view(np.uint64))
+
+
 @pytest.mark.parametrize("log_kb", [32, 38])
 def test_kb_float_quotient_boundary(ctx, oracle, log_kb):
     """The L units take Kb mod p from one float quotient while Kb =
