@@ -747,6 +747,8 @@ constexpr uint64_t kQuotErr38 = (1ull << (38 - 22)) / (TB + 1) + 1;  // Kb < 2^3
 static_assert((1ull << 32) / (TB + 1) < (1ull << kQuotBits), "Kb < 2^32: float quotient within 1 (and < 2^24 for __umul24)");
 static_assert((kQuotErr38 + 2) * kWheelMaxPrime < (1ull << 31), "Kb < 2^38: the rest Kb - q p must be exact in int32");
 static_assert(kWheelMaxPrime < (1ull << 23), "__mul24 / __umul24 operands and float-exact p");
+static_assert((uint64_t)(kWheelMaxPrime + 1) * (kWheelMaxPrime + 1) / 30 < (1ull << 38),
+              "ranges without bucketed primes never need the Barrett path (unit_L<false>)");
 
 // L: 64 large primes (p > TB), one per lane; at step q lane L handles the
 // absolute residue (q + L) & 7 (a half-wave spreads over all 8 planes). The
@@ -970,6 +972,11 @@ __device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, co
   }
 }
 
+// BARRETT: the launch may hold Kb >= 2^38 (values above 8.2e12, only with
+// bucketed primes: the ranges without them end below (2^20 + 1)^2 < 2^40, so
+// Kb < 2^36 there and the instantiation keeps no Barrett factors in its
+// operand registers)
+template <bool BARRETT>
 __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t Vend, uint64_t Kb,
                                        const PlaneSteps& ps, uint32_t pl_rot, uint64_t rho_pack) {
   const uint32_t p = o.p;
@@ -986,7 +993,7 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
     uint32_t x = (uint32_t)Kb - __umul24(q, p);  // in (-p, 2p) as a signed value; p < 2^24
     x = min(x, x + p);
     kbm = min(x, x - p);
-  } else if (Kb < (1ull << 38)) {
+  } else if (!BARRETT || Kb < (1ull << 38)) {
     // values below 8.2e12: the float quotient of Kb is within kQuotErr38 of
     // the true one (relative error < 2^-22, Kb / p < 2^38 / (TB + 1)), so
     // Kb - q p is exact in 32 bits (|.| < (kQuotErr38 + 1) p < 2^31, asserted
@@ -1372,7 +1379,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       ps.ne[q] = 0u - ((e_rot >> q) & 1u);
     }
     const uint64_t Kb = rg.KB0 + s * (uint64_t)KP;
-    const bool need_m = Kb >= (1ull << 38);  // unit_L's Barrett path
+    const bool need_m = BK && Kb >= (1ull << 38);  // unit_L's Barrett path (unit_L<BK>)
     MidRes mr;
     mr.x = lds.mid_x;
     mr.inc = lds.mid_inc;
@@ -1503,9 +1510,9 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         }
       } else {
         const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p);
-        if ((uint64_t)p0 * p0 < Vend) unit_L(cur, Vs, Vend, Kb, ps, pl_rot, rg.rho_pack);
+        if ((uint64_t)p0 * p0 < Vend) unit_L<BK>(cur, Vs, Vend, Kb, ps, pl_rot, rg.rho_pack);
         const uint32_t p1 = __builtin_amdgcn_readfirstlane(cur1.p);
-        if ((uint64_t)p1 * p1 < Vend) unit_L(cur1, Vs, Vend, Kb, ps, pl_rot, rg.rho_pack);
+        if ((uint64_t)p1 * p1 < Vend) unit_L<BK>(cur1, Vs, Vend, Kb, ps, pl_rot, rg.rho_pack);
       }
       cur = nxt;
       cur1 = nxt1;
