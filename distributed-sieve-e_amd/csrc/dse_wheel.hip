@@ -322,14 +322,34 @@ __device__ __forceinline__ void mark_tail(uint32_t pb4, uint32_t k, uint32_t p, 
       : "memory", "vcc");
 }
 
-// The rest of a walk known to be at most T (1 or 2) steps: T predicated marks,
+// The rest of a walk known to be at most T (1 to 4) steps: T predicated marks,
 // no loop (mark_tail's loop costs 2 more VALU and 2-3 branches for 1-2
 // steps). The second mark's lanes are a subset of the first's, so exec is
 // narrowed twice and restored once, all inside the block.
+#define DSE_TAIL_MARK                    \
+  "v_cmpx_gt_u32_e32 vcc, %5, %2\n\t" \
+  "v_and_or_b32 %0, %2, %6, %7\n\t"   \
+  "v_lshlrev_b32 %1, %2, %8\n\t"
+#define DSE_TAIL_STEP DSE_TAIL_MARK "v_add_u32 %2, %2, %4\n\t" "ds_or_b32 %0, %1\n\t"
+#define DSE_TAIL_LAST DSE_TAIL_MARK "ds_or_b32 %0, %1\n\t"
 template <int T>
 __device__ __forceinline__ void mark_tail_n(uint32_t pb4, uint32_t k, uint32_t p, uint32_t one) {
   uint64_t sv;
   uint32_t a, b;
+  if (T == 3 || T == 4) {
+    if (T == 3)
+      asm volatile("s_mov_b64 %3, exec\n\t" DSE_TAIL_STEP DSE_TAIL_STEP DSE_TAIL_LAST "s_mov_b64 exec, %3"
+                   : "=&v"(a), "=&v"(b), "+v"(k), "=&s"(sv)
+                   : "v"(p), "s"(KP), "s"(kBlockMask), "v"(pb4), "v"(one)
+                   : "memory", "vcc");
+    else
+      asm volatile("s_mov_b64 %3, exec\n\t" DSE_TAIL_STEP DSE_TAIL_STEP DSE_TAIL_STEP DSE_TAIL_LAST
+                   "s_mov_b64 exec, %3"
+                   : "=&v"(a), "=&v"(b), "+v"(k), "=&s"(sv)
+                   : "v"(p), "s"(KP), "s"(kBlockMask), "v"(pb4), "v"(one)
+                   : "memory", "vcc");
+    return;
+  }
   if (T == 1)
     asm volatile(
         "s_mov_b64 %3, exec\n\t"
@@ -950,7 +970,7 @@ __device__ __forceinline__ void start_marks4(const uint32_t* a, const uint32_t* 
         : "memory", "vcc");
 }
 
-// MODE 0 with TT = 1 or 2: at most TT hits per plane after the n_min run
+// MODE 0 with TT = 1..4: at most TT hits per plane after the n_min run
 // (mark_tail_n); TT = 0: the loop.
 template <int MODE, int TT = 0>
 __device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, const PlaneSteps& ps,
@@ -1029,6 +1049,8 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
           (uint32_t)__builtin_amdgcn_readfirstlane(div_ceil_small(KP, pmin, fast_rcp((float)pmin))) - n_min;
       if (pmax < KP && n_tail == 1) unit_L_fast<0, 1>(o, nKbm, ps, n_min);
       else if (pmax < KP && n_tail == 2) unit_L_fast<0, 2>(o, nKbm, ps, n_min);
+      else if (pmax < KP && n_tail == 3) unit_L_fast<0, 3>(o, nKbm, ps, n_min);
+      else if (pmax < KP && n_tail == 4) unit_L_fast<0, 4>(o, nKbm, ps, n_min);
       else unit_L_fast<0>(o, nKbm, ps, n_min);
     }
     return;
