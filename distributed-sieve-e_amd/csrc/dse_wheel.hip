@@ -323,9 +323,9 @@ __device__ __forceinline__ void mark_tail(uint32_t pb4, uint32_t k, uint32_t p, 
 }
 
 // The rest of a walk known to be at most T (1 to 4) steps: T predicated marks,
-// no loop (mark_tail's loop costs 2 more VALU and 2-3 branches for 1-2
-// steps). The second mark's lanes are a subset of the first's, so exec is
-// narrowed twice and restored once, all inside the block.
+// no loop (mark_tail's loop costs 2 more VALU and 2-3 branches per step).
+// Each mark's lanes are a subset of the previous mark's, so exec narrows with
+// every v_cmpx and is restored once, all inside the block.
 #define DSE_TAIL_MARK                    \
   "v_cmpx_gt_u32_e32 vcc, %5, %2\n\t" \
   "v_and_or_b32 %0, %2, %6, %7\n\t"   \
