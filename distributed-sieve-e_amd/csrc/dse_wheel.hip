@@ -1302,6 +1302,13 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       const uint4 ra = rp[hi_first ? 1 : 0], rb = rp[hi_first ? 0 : 1];
       const uint4 lo = hi_first ? rb : ra, hi = hi_first ? ra : rb;
       uint32_t W[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};  // composite bits of planes 0..7
+      // composite candidates of the block's 256 (8 planes x 32 periods), from
+      // the raw words (the transpose keeps it): 8 v_bcnt instead of 15 over
+      // the output words; the range's first block (small primes put back by
+      // rg.fix) and its end count the output instead
+      uint32_t n_comp = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) n_comp += __popc(W[j]);
       // Transpose every byte column of the 8 x 32 bit matrix in place (rows =
       // planes): afterwards W[j] byte q bit i = plane i, period 8q + j.
       bit_block_swaps(W);
@@ -1334,8 +1341,12 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       const uint64_t bit0 = 32ull * w0;
       if (bit0 + 480 <= rg.nbits) {  // whole block inside the range (a separate path: no phi copies of o[])
         uint32_t cnt = 0;
+        if (s == 0 && blk == 0) {
 #pragma unroll
-        for (int w = 0; w < 15; ++w) cnt += __popc(o[w]);
+          for (int w = 0; w < 15; ++w) cnt += __popc(o[w]);
+        } else {
+          cnt = 256u - n_comp;
+        }
         my_count += cnt;
         if (out) {
 #pragma unroll
