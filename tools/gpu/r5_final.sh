@@ -2,7 +2,7 @@
 # config sweep, rank steps, rocprofv3 trace + PMC of the bench, extra PMC groups, window kernel stats,
 # A/B against the round-start build.
 set -o pipefail
-O=gpurun_out/ev5e
+O=gpurun_out/ev5f
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gputest.log 2>&1 || { tail -30 $O/gputest.log; exit 1; }
 tail -1 $O/gputest.log
