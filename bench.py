@@ -23,10 +23,13 @@ Prints ONE JSON line on rank 0.
 from __future__ import annotations
 
 import argparse
+import datetime
+import faulthandler
 import json
 import os
 import statistics
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -186,11 +189,56 @@ def lds_instr_check(wm: int, cs: int, pmc):
             "unit": "LDS wave-instructions per launch"}
 
 
+class Watchdog:
+    """A stuck rank must end the run with a diagnosable non-zero exit, not run
+    into the driver's time limit: every phase (rendezvous, warmup, timed steps,
+    gather of the per-rank figures ...) has a deadline; past it the rank
+    prints its rank, world size and phase and every thread's stack to stderr
+    and exits with status 3. Collectives also carry the process group's
+    timeout (init_process_group(timeout=...)). DSE_BENCH_PHASE_TIMEOUT_S
+    (default 300) sets both."""
+
+    def __init__(self, rank: int, world: int, limit_s: float):
+        self.rank, self.world, self.limit = rank, world, limit_s
+        self.name, self.t0 = "start", time.monotonic()
+        self.lock = threading.Lock()
+        threading.Thread(target=self._run, daemon=True).start()
+
+    def phase(self, name: str) -> None:
+        with self.lock:
+            self.name, self.t0 = name, time.monotonic()
+
+    def where(self) -> str:
+        return f"bench.py rank {self.rank}/{self.world} in phase '{self.name}'"
+
+    def _run(self):
+        while True:
+            time.sleep(1.0)
+            with self.lock:
+                late = time.monotonic() - self.t0 > self.limit
+                msg = f"{self.where()}: no progress for {self.limit:.0f} s, exiting"
+            if late:
+                print(msg, file=sys.stderr, flush=True)
+                faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
+                sys.stderr.flush()
+                os._exit(3)
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    wd = Watchdog(rank, world, float(os.environ.get("DSE_BENCH_PHASE_TIMEOUT_S", "300")))
+    try:
+        run(a, world, rank, wd)
+    except BaseException as e:  # noqa: BLE001 -- name the rank and phase, then re-raise
+        print(f"{wd.where()}: {type(e).__name__}: {e}", file=sys.stderr, flush=True)
+        raise
+
+
+def run(a, world: int, rank: int, wd: Watchdog):
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    timeout = datetime.timedelta(seconds=wd.limit)
     # DSE_BENCH_REHEARSE=1: rehearsal of the N-rank code path on a 1-GPU box
     # (gloo, every rank on cuda:0); its timings mean nothing.
     rehearse = os.environ.get("DSE_BENCH_REHEARSE") == "1"
@@ -199,14 +247,15 @@ def main():
     if a.rccl_single and world != 1:
         sys.exit("--rccl-single is for a one-process run")
     pg = world > 1 or a.rccl_single  # the step's collectives run through a process group
+    wd.phase("init_process_group")
     if world > 1:
         if rehearse:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=timeout)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=timeout)
     elif a.rccl_single:
         dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1,
-                                device_id=torch.device("cuda", local))
+                                device_id=torch.device("cuda", local), timeout=timeout)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     P = world  # one spread-work chunk (or window slice) per GPU
@@ -231,16 +280,24 @@ def main():
     # the world this run formed (a SCALE line shows its N ranks and their devices)
     me = {"rank": rank, "local_rank": local, "device": torch.cuda.current_device(),
           "pci_bus_id": getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", None)}
+    wd.phase("gather rank info")
     ranks = [me]
     if world > 1:
         ranks = [None] * world
         dist.all_gather_object(ranks, me)
-    world_info = {"backend": dist.get_backend() if pg else None, "size": world, "ranks": ranks,
-                  "rehearsal": rehearse, "rccl_single": a.rccl_single}
-
     ctx = S.Context(device=local)
     tbytes = S.base_table_bytes(limit)
-    pbytes = S.base_table_prime_bytes(limit)  # the primes: all a broadcast needs to carry
+    # the primes are all a broadcast needs to carry (109 KB at N=1e11); a table
+    # past the broadcast cap (the window's 203 MB) is built on every rank
+    # instead (include/dse.h dse_base_table_broadcast_bytes)
+    pbytes = S.base_table_broadcast_bytes(limit)
+    share = "broadcast" if pbytes else "local"
+    world_info = {"backend": dist.get_backend() if pg else None, "size": world, "ranks": ranks,
+                  "rehearsal": rehearse, "rccl_single": a.rccl_single,
+                  "base_table": {"limit": limit, "path": share,
+                                 "bytes": pbytes if pbytes else S.base_table_prime_bytes(limit),
+                                 "rule": "rank 0 builds and broadcasts the primes while they fit in 8 MiB; "
+                                         "above that every rank builds its own table"}}
     table = torch.empty(tbytes, dtype=torch.uint8, device=dev)
     counts = torch.zeros(2, dtype=torch.int64, device=dev)
     mask = torch.empty(words, dtype=torch.int64, device=dev) if with_mask else None
@@ -250,9 +307,9 @@ def main():
 
     def launch(timed=False):
         counts.zero_()
-        if rank == 0:
+        if rank == 0 or not pbytes:
             ctx.base_primes_dev_async(limit, table.data_ptr(), tbytes, sp)
-        if pg:
+        if pg and pbytes:
             dist.broadcast(table[:pbytes], src=0)
             if rank != 0:
                 ctx.base_table_finish_dev_async(limit, table.data_ptr(), tbytes, sp)
@@ -279,11 +336,13 @@ def main():
     def barrier():
         torch.cuda.synchronize()
         if world > 1:
-            dist.barrier()
+            dist.barrier(device_ids=None if rehearse else [local])
 
+    wd.phase("warmup")
     for _ in range(a.warmup):
         step()
     barrier()
+    wd.phase("timed steps")
     t0 = time.perf_counter()
     step_s = []
     for _ in range(a.steps):
@@ -292,6 +351,7 @@ def main():
     barrier()
     t1 = time.perf_counter()
     # back-to-back launches without host round trips (the r01 headline method)
+    wd.phase("pipelined steps")
     barrier()
     tp0 = time.perf_counter()
     for _ in range(a.steps):
@@ -299,12 +359,24 @@ def main():
     barrier()
     tp1 = time.perf_counter()
 
+    wd.phase("reduce timings")
     step_t = torch.tensor(step_s + [t1 - t0, tp1 - tp0], dtype=torch.float64, device=dev)
     kern = sum(e0.elapsed_time(e1) for e0, e1 in kev) / len(kev) / 1e3  # s per sieve launch
     kern_t = torch.tensor([kern], dtype=torch.float64, device=dev)
+    # this rank's own figures, next to its device in world.ranks (a SCALE line
+    # can then be checked rank by rank against profiles/*/rank_steps.txt)
+    mine = {"step_ms": statistics.median(step_s) * 1e3, "kernel_ms": kern * 1e3,
+            "bracketed_ms": (t1 - t0) / a.steps * 1e3, "pipelined_ms": (tp1 - tp0) / a.steps * 1e3,
+            "g_start": g0, "nbits": cs, "tail_nbits": tail_n if rank == world - 1 else 0}
+    per_rank = [mine]
     if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
         dist.all_reduce(step_t, op=dist.ReduceOp.MAX)
         dist.all_reduce(kern_t, op=dist.ReduceOp.MAX)
+    for r, x in zip(ranks, per_rank):
+        r.update(x)
+    wd.phase("report")
     st = step_t.cpu().tolist()
     med = statistics.median(st[:a.steps])
     bracketed, pipelined = st[a.steps] / a.steps, st[a.steps + 1] / a.steps
@@ -402,8 +474,10 @@ def main():
                 },
             }
         if world == 1 and a.cpu_baseline == "on" and not a.window:
+            wd.phase("cpu baseline")
             out["cpu_baseline"] = cpu_baseline(int(a.cpu_max_n))
         print(json.dumps(out), flush=True)
+    wd.phase("shutdown")
     ctx.close()
     if pg:
         dist.destroy_process_group()

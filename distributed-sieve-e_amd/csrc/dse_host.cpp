@@ -96,6 +96,7 @@ struct dse_ctx {
   // grouped ncclBroadcast / ncclAllReduce on a one-GPU box.
   bool rccl_single = false;
   int64_t rccl_calls = 0;                  // collectives RCCL accepted (dse_debug_get_stat)
+  int64_t table_local_builds = 0;          // tables built per device instead of broadcast (share_table)
   unsigned long long* lg_stage = nullptr;  // gathered counts [devs][n]
   unsigned long long* lg_sum = nullptr;    // their sum [n]
   uint64_t lg_n = 0;                       // n of the two buffers
@@ -189,13 +190,26 @@ int32_t init_dev(DevState& d, int device) {
 // factors and wheel offsets locally: the reference's prime broadcast
 // (sieve.clj:139, core.clj:94-95,126) done once. Every device's table buffer
 // must already hold dse_base_table_bytes(limit) bytes.
+// A table whose primes exceed the broadcast cap (dse_base_table_broadcast_bytes:
+// the window's 203 MB) is built on every device instead, each on its own
+// stream: 0.2 ms of local work against 0.7-2 ms of broadcast (DESIGN.md
+// section 5). The test option table_broadcast_max_bytes moves the cap.
 int32_t share_table(dse_ctx* ctx, uint64_t limit) {
   int32_t rc;
+  const int nd = (int)ctx->devs.size();
+  const uint64_t pbytes = dse_base_table_prime_bytes(limit);
+  const uint64_t cap = ctx->opts.table_bcast_max ? ctx->opts.table_bcast_max : DSE_TABLE_BROADCAST_MAX_BYTES;
+  if ((nd > 1 || ctx->rccl_single) && pbytes > cap) {
+    for (int i = 0; i < nd; ++i) {
+      HIP_TRY(hipSetDevice(ctx->devs[i].device));
+      if ((rc = build_table(ctx->devs[i], limit))) return rc;
+    }
+    ctx->table_local_builds += nd;
+    return DSE_OK;
+  }
   HIP_TRY(hipSetDevice(ctx->devs[0].device));
   if ((rc = build_table(ctx->devs[0], limit))) return rc;
-  const int nd = (int)ctx->devs.size();
   if (nd == 1 && !ctx->rccl_single) return DSE_OK;
-  const uint64_t pbytes = dse_base_table_prime_bytes(limit);
   if (ctx->logical) {  // the broadcast as copies from device 0's table, each on its device's stream
     DevState& r = ctx->devs[0];
     HIP_TRY(hipEventRecord(r.xev, r.stream));
@@ -435,6 +449,11 @@ int32_t dse_base_primes_dev_async(dse_ctx* ctx, uint64_t limit, void* table_dev,
 }
 
 uint64_t dse_base_table_prime_bytes(uint64_t limit) { return 16ull + 4ull * prime_cap(limit); }
+
+uint64_t dse_base_table_broadcast_bytes(uint64_t limit) {
+  const uint64_t pbytes = dse_base_table_prime_bytes(limit);
+  return pbytes <= DSE_TABLE_BROADCAST_MAX_BYTES ? pbytes : 0;
+}
 
 int32_t dse_base_table_finish_dev_async(dse_ctx* ctx, uint64_t limit, void* table_dev, uint64_t table_bytes,
                                         void* stream) {
@@ -700,7 +719,11 @@ int32_t dse_debug_set_option(dse_ctx* ctx, const char* name, int64_t value) {
     return DSE_OK;
   }
   if (n == "bucket_lo_log2") {
-    if (value != 0 && (value < 17 || value > 20)) return fail(DSE_EINVAL, "bucket_lo_log2 must be 0 or 17..20");
+    // primes above 2^value are bucketed; those up to it go to the wheel kernel's
+    // L units, which hold primes <= kWheelMaxPrime only: a larger value would
+    // leave (kWheelMaxPrime, 2^value] in neither place
+    if (value != 0 && (value < 17 || value > DSE_WHEEL_MAX_LOG))
+      return fail(DSE_EINVAL, "bucket_lo_log2 must be 0 or 17.." + std::to_string(DSE_WHEEL_MAX_LOG));
     ctx->opts.bucket_lo_log2 = (uint32_t)value;
     return DSE_OK;
   }
@@ -723,6 +746,11 @@ int32_t dse_debug_set_option(dse_ctx* ctx, const char* name, int64_t value) {
     ctx->rccl_single = value == 1;
     return DSE_OK;
   }
+  if (n == "table_broadcast_max_bytes") {
+    if (value < 0) return fail(DSE_EINVAL, "table_broadcast_max_bytes must be >= 0");
+    ctx->opts.table_bcast_max = (uint64_t)value;
+    return DSE_OK;
+  }
   if (n == "bucket_cap_divisor") {
     if (value < 0 || value > 0xFFFFFFFFll) return fail(DSE_EINVAL, "bucket_cap_divisor out of range");
     ctx->opts.bucket_cap_div = (uint32_t)value;
@@ -736,6 +764,10 @@ int32_t dse_debug_get_stat(dse_ctx* ctx, const char* name, int64_t* value) {
   const std::string n(name);
   if (n == "rccl_calls") {
     *value = ctx->rccl_calls;
+    return DSE_OK;
+  }
+  if (n == "table_local_builds") {
+    *value = ctx->table_local_builds;
     return DSE_OK;
   }
   if (n == "rccl_comms") {

@@ -79,7 +79,8 @@ struct SieveOpts {
   uint32_t bucket_k0_div = 0;     // > 1: divide the band-0 region capacity, to test the spill list
   uint32_t wheel_geometry = 0;    // ranges without buckets: 0 auto (half-size tail), 1 full only, 2 half only
   uint32_t scratch_poison = 0;    // 1: fill the bucket scratch with 0xFF bytes before every pass (stale contents)
-  uint32_t bucket_lo_log2 = 0;    // k in 17..20: bucketed ranges bucket the primes above 2^k (0: production)
+  uint32_t bucket_lo_log2 = 0;    // k in 17..kWheelMaxLog: bucketed ranges bucket the primes above 2^k (0: production)
+  uint64_t table_bcast_max = 0;   // > 0: broadcast cap of share_table in bytes (0: DSE_TABLE_BROADCAST_MAX_BYTES)
 };
 
 hipError_t launch_base_primes(uint64_t limit, void* table, uint32_t cap, hipStream_t stream);

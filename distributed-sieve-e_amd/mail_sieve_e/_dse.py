@@ -51,6 +51,7 @@ SIGNATURES = {
     "dse_base_limit_for_range": (_u64, [_u64, _u64]),
     "dse_base_primes_dev_async": (_i32, [_vp, _u64, _vp, _u64, _vp]),
     "dse_base_table_prime_bytes": (_u64, [_u64]),
+    "dse_base_table_broadcast_bytes": (_u64, [_u64]),
     "dse_base_table_finish_dev_async": (_i32, [_vp, _u64, _vp, _u64, _vp]),
     "dse_sieve_range_dev_async": (_i32, [_vp, _vp, _u64, _u64, _vp, _vp, _vp]),
     "dse_device_status": (_i32, [_vp]),

@@ -144,6 +144,14 @@ def base_table_prime_bytes(limit: int) -> int:
     return int(lib().dse_base_table_prime_bytes(limit))
 
 
+def base_table_broadcast_bytes(limit: int) -> int:
+    """Bytes rank 0 broadcasts for a table of odd primes <= limit, or 0 when
+    every rank builds its own table (include/dse.h dse_base_table_broadcast_bytes:
+    the primes move while they fit in 8 MiB; the 1e18 window's 203 MB are
+    rebuilt on every device, which is faster than moving them)."""
+    return int(lib().dse_base_table_broadcast_bytes(limit))
+
+
 def base_limit_for_range(g_start: int, nbits: int) -> int:
     return int(lib().dse_base_limit_for_range(g_start, nbits))
 

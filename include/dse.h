@@ -154,6 +154,17 @@ int32_t dse_base_primes_dev_async(dse_ctx *ctx, uint64_t limit, void *table_dev,
  * dse_base_table_finish_dev_async. */
 uint64_t dse_base_table_prime_bytes(uint64_t limit);
 
+/* How ranks should share the base table for `limit`: the bytes to broadcast
+ * from rank 0 (dse_base_table_prime_bytes(limit)), or 0 when every rank should
+ * build its own table with dse_base_primes_dev_async instead. The primes are
+ * broadcast (as the reference broadcasts them, sieve.clj:139) while they fit
+ * in DSE_TABLE_BROADCAST_MAX_BYTES; a larger table (the 1e18 window's 50.8 M
+ * primes, 203 MB) is rebuilt on every device, which takes less time than
+ * moving it. dse_sieve_all / dse_sieve_window follow
+ * the same rule. */
+#define DSE_TABLE_BROADCAST_MAX_BYTES (8ull << 20)
+uint64_t dse_base_table_broadcast_bytes(uint64_t limit);
+
 /* Complete a table of odd primes <= limit whose first
  * dse_base_table_prime_bytes(limit) bytes are in place (e.g. received by
  * broadcast): Barrett factors and mod-30 wheel offsets, on this context's
@@ -196,9 +207,14 @@ int32_t dse_device_status(dse_ctx *ctx);
  *   "scratch_poison" = 1: fill the bucket scratch with 0xFF bytes before
  *   every bucketed pass (stale contents: results unchanged, and an overflowed
  *   pass still reads only what it wrote); 0 = default.
- *   "bucket_lo_log2" = k in 17..20: a range that needs the bucketed pass
- *   (sqrt of its largest value above 2^20) buckets every prime above 2^k
- *   instead of the production threshold; 0 = default.
+ *   "bucket_lo_log2" = k in 17..20 (at most the build's wheel limit, 2^20 in
+ *   production): a range that needs the bucketed pass (sqrt of its largest
+ *   value above 2^20) buckets every prime above 2^k instead of the production
+ *   threshold; 0 = default.
+ *   "table_broadcast_max_bytes" = b > 0: dse_sieve_all / dse_sieve_window
+ *   broadcast the table's primes while they take at most b bytes and build
+ *   the table on every device above that; 0 = default
+ *   (DSE_TABLE_BROADCAST_MAX_BYTES).
  *   "rccl_single" = 1: give a one-device context (dse_init(1) or
  *   dse_init_device) a 1-rank RCCL communicator (ncclCommInitAll), so
  *   dse_sieve_all / dse_sieve_window issue the same grouped ncclBroadcast of
@@ -211,7 +227,9 @@ int32_t dse_debug_set_option(dse_ctx *ctx, const char *name, int64_t value);
 /* Read a test-only statistic of this context into *value:
  *   "rccl_calls": RCCL collectives (one per device and call) accepted so far;
  *   "rccl_comms": communicators the context holds;
- *   "rccl_ranks": ranks of its communicator as ncclCommCount reports (0: none).
+ *   "rccl_ranks": ranks of its communicator as ncclCommCount reports (0: none);
+ *   "table_local_builds": base tables built on a device of their own instead
+ *   of broadcast (one per device and call).
  * DSE_EINVAL for an unknown name. */
 int32_t dse_debug_get_stat(dse_ctx *ctx, const char *name, int64_t *value);
 

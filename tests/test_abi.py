@@ -72,6 +72,20 @@ def test_base_limits():
     assert S.base_table_bytes(10**6) >= 16 + 12 * 78497
 
 
+def test_table_broadcast_rule():
+    """Chunk configs broadcast the primes (the reference's broadcast,
+    sieve.clj:139): 1e11 and 1e12 tables are 109 KB / 314 KB; the 1e18
+    window's table (limit 1e9 + 4, 203 MB) is built on every device instead."""
+    from mail_sieve_e import sieve as S
+    for n in (10**9, 10**10, 10**11, 10**12):
+        lim = S.base_limit_for_range(0, (n - 1) // 2)
+        assert S.base_table_broadcast_bytes(lim) == S.base_table_prime_bytes(lim) <= 8 << 20
+    g = (10**18 + 1 - 3) // 2
+    lim = S.base_limit_for_range(g, 10**10 // 2)
+    assert lim == 10**9 + 4 and S.base_table_prime_bytes(lim) > 200e6
+    assert S.base_table_broadcast_bytes(lim) == 0
+
+
 def test_no_gpu_init_fails_cleanly():
     from mail_sieve_e import _dse
     L = _dse.lib()

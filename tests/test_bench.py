@@ -33,6 +33,15 @@ def _check_line(d: dict, n_gpus: int):
     # the world the run formed: one entry per rank
     w = d["world"]
     assert w["size"] == n_gpus and [x["rank"] for x in w["ranks"]] == list(range(n_gpus))
+    # every rank's own figures (all-gathered, not only the max), so an N-GPU
+    # line can be checked rank by rank; the headline is the max over ranks
+    for x in w["ranks"]:
+        assert x["step_ms"] > 0 and x["kernel_ms"] > 0 and x["bracketed_ms"] > 0 and x["pipelined_ms"] > 0
+        assert x["nbits"] == d["config"]["cs"]
+    assert sorted(x["g_start"] for x in w["ranks"]) == [r * d["config"]["cs"] for r in range(n_gpus)]
+    assert abs(d["roofline"]["kernel_ms"] - max(x["kernel_ms"] for x in w["ranks"])) < 1e-9 + 1e-9 * d["roofline"]["kernel_ms"]
+    # chunk configs broadcast the primes (109 KB at 1e11, the reference's broadcast)
+    assert w["base_table"]["path"] == "broadcast" and 0 < w["base_table"]["bytes"] <= 8 << 20
     # the headline is the median of per-step times, each from the call to the counts on the host
     assert d["ms_per_step"] > 0 and d["ms_per_step_bracketed"] > 0 and d["ms_per_step_pipelined"] > 0
     assert abs(d["value"] - d["config"]["N"] / (d["ms_per_step"] / 1e3)) < 1e-6 * d["value"]
@@ -68,6 +77,10 @@ def test_bench_window_two_rank_rehearsal():
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 2 and d["verified"] is True and d["pi_full"] == 241272176
     assert d["config"]["P"] == 2 and d["value"] > 0
+    # the window's 203 MB of primes are not broadcast: every rank builds its table
+    t = d["world"]["base_table"]
+    assert t["path"] == "local" and t["bytes"] > 8 << 20
+    assert [x["rank"] for x in d["world"]["ranks"]] == [0, 1] and all(x["kernel_ms"] > 0 for x in d["world"]["ranks"])
 
 
 @pytest.mark.gpu
@@ -100,3 +113,14 @@ def test_bench_single_rank_rccl_line():
     _check_line(d, 1)
     assert d["world"]["backend"] == "nccl" and d["world"]["rccl_single"] is True
     assert d["pi_full"] == 455052511
+
+
+def test_watchdog_names_rank_and_phase():
+    """A stuck phase ends the rank with status 3 and its rank, world size and
+    phase on stderr (bench.Watchdog), instead of running into the driver's
+    time limit. CPU only: no GPU call is made."""
+    code = ("import sys, time; sys.path.insert(0, %r); import bench; "
+            "w = bench.Watchdog(1, 8, 1.0); w.phase('timed steps'); time.sleep(30)" % ROOT)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert "bench.py rank 1/8 in phase 'timed steps': no progress for 1 s" in r.stderr

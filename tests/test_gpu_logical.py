@@ -61,7 +61,7 @@ def test_1e11_p8_golden_on_8_logical_devices(S):
         counts, pi_ref, pi_full = c.sieve_all(10**11, 8)
         assert pi_ref == pi_full == 4_118_054_813
         assert [int(x) for x in counts] == g["counts"]
-        for k in (1, 8):
+        for k in range(1, 9):
             assert sha(c.copy_chunk_mask(10**11, 8, k)) == g["mask_sha256"][k - 1], k
 
 
@@ -74,8 +74,11 @@ def test_1e12_p8_on_8_logical_devices(S):
         counts, pi_ref, pi_full = c.sieve_all(10**12, 8)
         assert pi_ref == 37_607_912_017
         assert pi_full == 37_607_912_018
-        if g is not None:
-            assert [int(x) for x in counts] == g["counts"]
+        assert g is not None
+        assert [int(x) for x in counts] == g["counts"]
+        # chunk 8 (values 8.75e11 .. 1e12, on the last device) is the 8-GPU
+        # critical path: every large prime live in every segment
+        assert sha(c.copy_chunk_mask(10**12, 8, 8)) == g["mask_sha256"][7]
 
 
 def test_window_on_logical_devices(S, oracle):
@@ -89,10 +92,20 @@ def test_window_on_logical_devices(S, oracle):
             assert c.sieve_window(lo, hi) == c1, nd
 
 
-def test_window_full_on_8_logical_devices(S):
-    """[1e18, 1e18+1e10] over 8 devices: 241,272,176 (oracle fast_count_window)."""
+@pytest.mark.parametrize("share", ["local", "broadcast"])
+def test_window_full_on_8_logical_devices(S, share):
+    """[1e18, 1e18+1e10] over 8 devices: 241,272,176 (oracle fast_count_window).
+    The table's 50.8 M primes (203 MB) exceed the broadcast cap, so by default
+    every device builds its own table (table_local_builds); with the cap
+    raised the primes take the broadcast path (copies from device 0 here)."""
     with S.Context(logical=8) as c:
+        if share == "broadcast":
+            c.debug_set_option("table_broadcast_max_bytes", 1 << 40)
         assert c.sieve_window(10**18, 10**18 + 10**10) == GOLDEN["big"]["window_1e18"]["count"] == 241_272_176
+        assert c.debug_get_stat("table_local_builds") == (8 if share == "local" else 0)
+        # chunk configs keep the broadcast (the reference's prime broadcast)
+        assert c.sieve_all(10**10, 8)[2] == 455_052_511
+        assert c.debug_get_stat("table_local_builds") == (8 if share == "local" else 0)
 
 
 def test_logical_rejects_bad_count(S):

@@ -60,13 +60,20 @@ def test_sieve_all_1e12_p8_through_rccl(S):
         assert c.debug_get_stat("rccl_calls") == 2
 
 
-def test_window_full_through_rccl(S):
-    """[1e18, 1e18+1e10]: the 50.8 M base primes broadcast by ncclBroadcast,
-    the count by ncclAllReduce: 241,272,176 (oracle fast_count_window)."""
+@pytest.mark.parametrize("share", ["local", "broadcast"])
+def test_window_full_through_rccl(S, share):
+    """[1e18, 1e18+1e10], the count by ncclAllReduce: 241,272,176 (oracle
+    fast_count_window). The 50.8 M base primes (203 MB) are past the
+    broadcast cap, so by default every device builds its own table and the
+    only collective is the all-reduce; with the cap raised they go through
+    ncclBroadcast as well."""
     with S.Context() as c:
         c.debug_set_option("rccl_single", 1)
+        if share == "broadcast":
+            c.debug_set_option("table_broadcast_max_bytes", 1 << 40)
         assert c.sieve_window(10**18, 10**18 + 10**10) == GOLDEN["big"]["window_1e18"]["count"] == 241_272_176
-        assert c.debug_get_stat("rccl_calls") == 2
+        assert c.debug_get_stat("rccl_calls") == (1 if share == "local" else 2)
+        assert c.debug_get_stat("table_local_builds") == (1 if share == "local" else 0)
 
 
 def test_rccl_single_off_again_and_rejections(S):
