@@ -63,6 +63,15 @@ constexpr uint32_t BLOCKS = KP / 32;        // 32-period blocks (8 words each)
 constexpr uint32_t IMG_WORDS = 8 * BLOCKS;  // one segment image
 constexpr uint32_t IMG_BYTES = 4 * IMG_WORDS;
 static_assert(IMG_BYTES == KP, "a period index is its block's byte address");
+// The image sits at the top of the workgroup's LDS, bytes [kImgOff, kImgOff +
+// IMG_BYTES) (WheelLds): mark addresses are image-relative (a period index |
+// its plane's offset) and every ds_or adds kImgOff in its offset field. A
+// mark at a period k >= KP (past the segment) thus lands at or beyond the end
+// of the allocation, where the LDS drops it (microbench/lds_oor_bench.hip);
+// nothing lives above the image. So marks that may fall past the segment's
+// end are issued unconditionally, without a compare and exec masking.
+#define DSE_IMG_OFF_S "32768"
+constexpr uint32_t kImgOff = 32768;
 constexpr uint32_t NT = 1024;
 constexpr uint32_t NW = NT / 64;            // waves; every wave marks, expands and inits
 static_assert(BLOCKS % (64 * NW) == 0, "expansion blocks");
@@ -225,6 +234,12 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x) {
 }
 
 constexpr uint32_t kBlockMask = ~31u;  // period index -> its block's byte address
+#ifndef DSE_SHORT_TAIL
+#define DSE_SHORT_TAIL 8
+#endif
+// MODE-0 L sets whose tail after the n_min run is at most this many steps mark
+// it unconditionally (past the segment: dropped) instead of in mark_tail's loop
+constexpr uint32_t kShortTail = DSE_SHORT_TAIL;
 
 // Mark period k (< KP) of the plane whose byte base is pb4 (image + 4 plane):
 // address (k & ~31) | pb4 in one v_and_or, bit 1 << (k & 31) (the shift reads
@@ -234,7 +249,7 @@ __device__ __forceinline__ void mark_k(uint32_t pb4, uint32_t k, uint32_t one) {
   asm volatile(
       "v_and_or_b32 %0, %2, %3, %4\n\t"
       "v_lshlrev_b32 %1, %2, %5\n\t"
-      "ds_or_b32 %0, %1"
+      "ds_or_b32 %0, %1 offset:" DSE_IMG_OFF_S
       : "=&v"(a), "=&v"(b)
       : "v"(k), "s"(kBlockMask), "v"(pb4), "v"(one)
       : "memory");
@@ -247,7 +262,7 @@ __device__ __forceinline__ void mark_k_step(uint32_t pb4, uint32_t& k, uint32_t 
   asm volatile(
       "v_and_or_b32 %0, %2, %3, %4\n\t"
       "v_lshlrev_b32 %1, %2, %6\n\t"
-      "ds_or_b32 %0, %1\n\t"
+      "ds_or_b32 %0, %1 offset:" DSE_IMG_OFF_S "\n\t"
       "v_add_u32 %2, %2, %5"
       : "=&v"(a), "=&v"(b), "+v"(k)
       : "s"(kBlockMask), "v"(pb4), "v"(p), "v"(one)
@@ -264,19 +279,19 @@ __device__ __forceinline__ void mark_k_step4(uint32_t pb4, uint32_t& k, uint32_t
       "v_and_or_b32 %0, %4, %5, %6\n\t"
       "v_lshlrev_b32 %1, %4, %8\n\t"
       "v_add_u32 %4, %4, %7\n\t"
-      "ds_or_b32 %0, %1\n\t"
+      "ds_or_b32 %0, %1 offset:" DSE_IMG_OFF_S "\n\t"
       "v_and_or_b32 %2, %4, %5, %6\n\t"
       "v_lshlrev_b32 %3, %4, %8\n\t"
       "v_add_u32 %4, %4, %7\n\t"
-      "ds_or_b32 %2, %3\n\t"
+      "ds_or_b32 %2, %3 offset:" DSE_IMG_OFF_S "\n\t"
       "v_and_or_b32 %0, %4, %5, %6\n\t"
       "v_lshlrev_b32 %1, %4, %8\n\t"
       "v_add_u32 %4, %4, %7\n\t"
-      "ds_or_b32 %0, %1\n\t"
+      "ds_or_b32 %0, %1 offset:" DSE_IMG_OFF_S "\n\t"
       "v_and_or_b32 %2, %4, %5, %6\n\t"
       "v_lshlrev_b32 %3, %4, %8\n\t"
       "v_add_u32 %4, %4, %7\n\t"
-      "ds_or_b32 %2, %3"
+      "ds_or_b32 %2, %3 offset:" DSE_IMG_OFF_S
       : "=&v"(a0), "=&v"(b0), "=&v"(a1), "=&v"(b1), "+v"(k)
       : "s"(kBlockMask), "v"(pb4), "v"(p), "v"(one)
       : "memory");
@@ -312,7 +327,7 @@ __device__ __forceinline__ void mark_tail(uint32_t pb4, uint32_t k, uint32_t p, 
       "v_and_or_b32 %0, %2, %6, %7\n\t"
       "v_lshlrev_b32 %1, %2, %8\n\t"
       "v_add_u32 %2, %2, %4\n\t"
-      "ds_or_b32 %0, %1\n\t"
+      "ds_or_b32 %0, %1 offset:" DSE_IMG_OFF_S "\n\t"
       "v_cmpx_gt_u32_e32 vcc, %5, %2\n\t"
       "s_cbranch_execnz 1b\n"
       "2:\n\t"
@@ -322,66 +337,9 @@ __device__ __forceinline__ void mark_tail(uint32_t pb4, uint32_t k, uint32_t p, 
       : "memory", "vcc");
 }
 
-// The rest of a walk known to be at most T (1 to 4) steps: T predicated marks,
-// no loop (mark_tail's loop costs 2 more VALU and 2-3 branches per step).
-// Each mark's lanes are a subset of the previous mark's, so exec narrows with
-// every v_cmpx and is restored once, all inside the block.
-#define DSE_TAIL_MARK                    \
-  "v_cmpx_gt_u32_e32 vcc, %5, %2\n\t" \
-  "v_and_or_b32 %0, %2, %6, %7\n\t"   \
-  "v_lshlrev_b32 %1, %2, %8\n\t"
-#define DSE_TAIL_STEP DSE_TAIL_MARK "v_add_u32 %2, %2, %4\n\t" "ds_or_b32 %0, %1\n\t"
-#define DSE_TAIL_LAST DSE_TAIL_MARK "ds_or_b32 %0, %1\n\t"
-template <int T>
-__device__ __forceinline__ void mark_tail_n(uint32_t pb4, uint32_t k, uint32_t p, uint32_t one) {
-  uint64_t sv;
-  uint32_t a, b;
-  if (T == 3 || T == 4) {
-    if (T == 3)
-      asm volatile("s_mov_b64 %3, exec\n\t" DSE_TAIL_STEP DSE_TAIL_STEP DSE_TAIL_LAST "s_mov_b64 exec, %3"
-                   : "=&v"(a), "=&v"(b), "+v"(k), "=&s"(sv)
-                   : "v"(p), "s"(KP), "s"(kBlockMask), "v"(pb4), "v"(one)
-                   : "memory", "vcc");
-    else
-      asm volatile("s_mov_b64 %3, exec\n\t" DSE_TAIL_STEP DSE_TAIL_STEP DSE_TAIL_STEP DSE_TAIL_LAST
-                   "s_mov_b64 exec, %3"
-                   : "=&v"(a), "=&v"(b), "+v"(k), "=&s"(sv)
-                   : "v"(p), "s"(KP), "s"(kBlockMask), "v"(pb4), "v"(one)
-                   : "memory", "vcc");
-    return;
-  }
-  if (T == 1)
-    asm volatile(
-        "s_mov_b64 %3, exec\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %5, %2\n\t"
-        "v_and_or_b32 %0, %2, %6, %7\n\t"
-        "v_lshlrev_b32 %1, %2, %8\n\t"
-        "ds_or_b32 %0, %1\n\t"
-        "s_mov_b64 exec, %3"
-        : "=&v"(a), "=&v"(b), "+v"(k), "=&s"(sv)
-        : "v"(p), "s"(KP), "s"(kBlockMask), "v"(pb4), "v"(one)
-        : "memory", "vcc");
-  else
-    asm volatile(
-        "s_mov_b64 %3, exec\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %5, %2\n\t"
-        "v_and_or_b32 %0, %2, %6, %7\n\t"
-        "v_lshlrev_b32 %1, %2, %8\n\t"
-        "v_add_u32 %2, %2, %4\n\t"
-        "ds_or_b32 %0, %1\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %5, %2\n\t"
-        "v_and_or_b32 %0, %2, %6, %7\n\t"
-        "v_lshlrev_b32 %1, %2, %8\n\t"
-        "ds_or_b32 %0, %1\n\t"
-        "s_mov_b64 exec, %3"
-        : "=&v"(a), "=&v"(b), "+v"(k), "=&s"(sv)
-        : "v"(p), "s"(KP), "s"(kBlockMask), "v"(pb4), "v"(one)
-        : "memory", "vcc");
-}
-
 // ds_or_b32 at a precomputed LDS byte address.
 __device__ __forceinline__ void mark_at(uint32_t a, uint32_t bit) {
-  asm volatile("ds_or_b32 %0, %1" : : "v"(a), "v"(bit) : "memory");
+  asm volatile("ds_or_b32 %0, %1 offset:" DSE_IMG_OFF_S : : "v"(a), "v"(bit) : "memory");
 }
 
 // The hits k + (r + 32 t) p, r = 0..31, t < K, of a lane that walks one
@@ -398,7 +356,7 @@ __device__ __forceinline__ void class_marks(uint32_t pb4, uint32_t k, uint32_t p
     asm volatile(
         "v_and_or_b32 %0, %2, %3, %4\n\t"
         "v_lshlrev_b32 %1, %2, %5\n\t"
-        "ds_or_b32 %0, %1"
+        "ds_or_b32 %0, %1 offset:" DSE_IMG_OFF_S
         : "=&v"(a), "=&v"(b)
         : "v"(k), "s"(kBlockMask), "v"(pb4), "v"(one)
         : "memory");
@@ -538,9 +496,9 @@ __device__ __forceinline__ void bit_block_swaps(uint32_t (&W)[8]) {
 // 256 = 32c + r, r = 0..31; class r's hits k0 + 256p t share their bit and
 // their byte addresses step by the wave-uniform 256p, so after 3 VALU of class
 // setup each further mark is one v_add. k0 = kp + (32c + r) p < 256p, so
-// every class has K = floor(KP / 256p) or K + 1 hits: K marks, then one
-// predicated by address < IMG_BYTES (exec mask). k = the class-0 hit of the
-// lane; the image is at LDS address 0.
+// every class has K = floor(KP / 256p) or K + 1 hits: K + 1 marks, the last
+// dropped past the image (address >= IMG_BYTES, see kImgOff). k = the class-0
+// hit of the lane.
 template <int K>
 __device__ __forceinline__ void a_classes(uint32_t pb4, uint32_t k, uint32_t p, uint32_t one) {
   const uint32_t D = p << 8;  // 256 p periods = bytes
@@ -557,7 +515,7 @@ __device__ __forceinline__ void a_classes(uint32_t pb4, uint32_t k, uint32_t p, 
       mark_at(a, bit);
       a += D;
     }
-    if (a < IMG_BYTES) mark_at(a, bit);
+    mark_at(a, bit);  // past the image (a >= IMG_BYTES): dropped
     k = opaque(k + p);
   }
 }
@@ -623,8 +581,8 @@ __device__ __forceinline__ void unit_A(uint32_t img0, uint32_t pi, uint64_t m, c
 // j = (L >> 3) & 3) owns the hits n with n mod 128 in [32j, 32j + 32), in
 // order: 32 marks k, k + p, ... then a jump of 96p. The four lanes of a plane
 // are 32p periods apart: distinct banks, as in A. The blocks of 128 hits
-// every lane fills are marked class by class (class_marks); the last one,
-// partly filled, in order with a per-lane count.
+// every lane fills are marked class by class (class_marks); the rest in
+// order with wave-uniform counts, the marks past the segment dropped.
 __device__ __forceinline__ void unit_B1(uint32_t img0, const uint32_t* __restrict__ s_mid_p,
                                         const uint64_t* __restrict__ s_mid_m, const MidRes& mr, uint32_t j0,
                                         uint32_t nj, uint64_t Vs, uint64_t rho_pack, uint32_t lane, uint32_t one) {
@@ -651,23 +609,26 @@ __device__ __forceinline__ void unit_B1(uint32_t img0, const uint32_t* __restric
   // class by class (hits 32j + r + 128t, t < tf: 128p periods apart, one
   // bit): 1 VALU per mark where walking them takes 3 (1e11: -0.9%)
   const uint32_t tf = (KP / pmax) / 128;  // wave-uniform (a scalar division)
-  const uint32_t skip = 96 * p;
   class_marks_k(tf, pb4, k, p, 128 * p, one);
   k += tf * (128 * p);
-  // the rest: ceil((KP - k) / p) hits left in this lane's next blocks of 32
-  while (k < KP) {
-    const uint32_t left = div_ceil_small(KP - k, p, invp);
-    const uint32_t n = min(left, 32u);
-    for (uint32_t r = 0; r < n; ++r) mark_k_step(pb4, k, p, one);
-    k += skip;
+  // the rest: every hit index n of either prime is below n_all = ceil(KP /
+  // pmin) (kp < p), so in each further block of 128 hits lane j marks hits
+  // base + 32j + r, r < min(32, n_all - base), in order; the ones past the
+  // segment are dropped (kImgOff). Wave-uniform counts, no per-lane loop.
+  const uint32_t pmin = __builtin_amdgcn_readfirstlane(p);
+  const uint32_t n_all = __builtin_amdgcn_readfirstlane(div_ceil_small(KP, pmin, fast_rcp((float)pmin)));
+  for (uint32_t base = 128 * tf; base < n_all; base += 128) {
+    mark_run(pb4, k, p, min(32u, n_all - base), one);
+    k += 128 * p;
   }
 }
 
 // B2: 8 mid primes (TB1 < p <= TB) x 8 planes; lane (prime L >> 3, plane
 // L & 7) marks its plane's hits: n_u unconditional marks for every lane (the
-// first 32 floor(n_u / 32) class by class, the rest in order), then a short
-// per-lane tail. A plane's lanes hold different primes, so their banks
-// collide at random (the L pattern).
+// first 32 floor(n_u / 32) class by class), then the rest and the tail up to
+// ceil(KP / pmin) hits as one run (the marks past the segment dropped). A
+// plane's lanes hold different primes, so their banks collide at random (the
+// L pattern).
 __device__ __forceinline__ void unit_B2(uint32_t img0, const uint32_t* __restrict__ s_mid_p,
                                         const uint64_t* __restrict__ s_mid_m, const MidRes& mr, uint32_t j0,
                                         uint32_t nj, uint64_t Vs, uint64_t Vend, uint64_t rho_pack, uint32_t lane,
@@ -695,8 +656,15 @@ __device__ __forceinline__ void unit_B2(uint32_t img0, const uint32_t* __restric
   const uint32_t K = n_u / 32;
   class_marks_k(K, pb4, k, p, 32 * p, one);
   k += K * (32 * p);
-  k = mark_run(pb4, k, p, n_u - 32 * K, one);
-  mark_tail(pb4, k, p, one);
+  if (any_slow) {
+    mark_tail(pb4, mark_run(pb4, k, p, n_u - 32 * K, one), p, one);
+    return;
+  }
+  // every lane has fewer than n_all = ceil(KP / pmin) hits (k < p): the rest
+  // as one run, the marks past the segment dropped (kImgOff)
+  const uint32_t pmin = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
+  const uint32_t n_all = __builtin_amdgcn_readfirstlane(div_ceil_small(KP, pmin, fast_rcp((float)pmin)));
+  mark_run(pb4, k, p, n_all - 32 * K, one);
 }
 
 // Operands of one large unit, loaded ahead of use. The table row of prime i
@@ -719,33 +687,6 @@ __device__ __forceinline__ void load_L(LargeOps& o, const uint32_t* __restrict__
   o.a[4] = hi.x; o.a[5] = hi.y; o.a[6] = hi.z; o.a[7] = hi.w;
 }
 
-// Mark plane-relative period kk of plane byte base pb4 = image + 4 * plane
-// (mark_k: 2 VALU). PRED: only if kk < KP -- a lane without a hit leaves the
-// ds_or (exec mask), so it adds no bank conflict (an OR of 0 at a random
-// block conflicts like a mark).
-template <bool PRED>
-__device__ __forceinline__ void mark_plane(uint32_t pb4, uint32_t kk, uint32_t one) {
-  if (PRED) {
-    // exec &= (kk < KP) for the one mark, restored after it: 1 VALU + 2 SALU
-    // where the compiler's if takes a compare, saveexec, branch and restore
-    // (1e12: -2.2%, profiles/r04/ab_threshold_grid2_1e12.txt)
-    uint64_t sv;
-    uint32_t a, b;
-    asm volatile(
-        "s_mov_b64 %0, exec\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %3, %4\n\t"
-        "v_and_or_b32 %1, %4, %5, %6\n\t"
-        "v_lshlrev_b32 %2, %4, %7\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %0"
-        : "=&s"(sv), "=&v"(a), "=&v"(b)
-        : "s"(KP), "v"(kk), "s"(kBlockMask), "v"(pb4), "v"(one)
-        : "memory", "vcc");
-    return;
-  }
-  mark_k(pb4, kk, one);
-}
-
 // Mark a bucketed hit: entry = LDS word index << 5 | bit (bucket_entry), so
 // the address is img0 + (e >> 5) * 4 and the bit 1 << (e & 31) (the shift
 // reads the low 5 bits itself): 3 VALU.
@@ -755,7 +696,7 @@ __device__ __forceinline__ void mark_entry(uint32_t img0, uint32_t e, uint32_t o
       "v_lshrrev_b32 %0, 3, %2\n\t"
       "v_and_or_b32 %0, %0, -4, %4\n\t"
       "v_lshlrev_b32 %1, %2, %3\n\t"
-      "ds_or_b32 %0, %1"
+      "ds_or_b32 %0, %1 offset:" DSE_IMG_OFF_S
       : "=&v"(a), "=&v"(b)
       : "v"(e), "v"(one), "v"(img0)
       : "memory");
@@ -797,198 +738,70 @@ __device__ __forceinline__ uint32_t plane_start(uint32_t a, uint32_t nKbm, uint3
 
 // Branch-free body of an L unit whose 64 primes are all live and past p^2
 // (the common case): the mark count per plane is decided once per unit.
-// MODE 2: pmin > KP, one predicated mark per plane; MODE 1: pmin > KP/2, two;
-// MODE 3: MODE 1 with pmax < KP, whose first mark every lane has (kk < p < KP),
-// so only the second is predicated; MODE 0: n_min unconditional marks per
-// plane and a short loop for the rest.
-// MODE 1/2: four planes per block, each a plane start (a - Kb - e) mod p and
-// its NM = 1 or 2 predicated marks kk, kk + p (NM = 3: two, the first
-// unconditional); a plane's second mark's lanes
-// are a subset of its first's, so exec is narrowed twice and restored once
-// per plane, from the copy the block saved on entry. Every exec write is
-// inside the block, so no code the compiler places between blocks can run
-// with a narrowed exec. 6 (10) VALU + 1 SALU per plane (one plane per block,
-// the r04 form, adds an exec save and the compiler's s_nop between two asm
-// blocks per plane: 1e12 +0.7%).
+// MODE 2: pmin > KP, one mark per plane; MODE 1: pmin > KP/2, two; MODE 0:
+// n_min unconditional marks per plane and a short loop for the rest. Marks
+// past the segment's end are dropped by the LDS (kImgOff), so MODE 1/2 and
+// short MODE-0 tails need no compare and no exec masking.
+// MODE 1/2: four planes per asm block, each a plane start (a - Kb - e) mod p
+// and its NM = 1 or 2 marks kk, kk + p: 5 VALU + one ds_or per mark (round
+// 5 predicated each mark with v_cmpx and restored exec after each plane: 2
+// instructions more per plane and one per block). One block of four planes,
+// not one per plane: between two asm blocks the compiler places an s_nop when
+// the second reads a VGPR the first wrote.
+#define DSE_PLANE_START(A, NE)                                       \
+  "v_add3_u32 %0, " A ", %15, " NE "\n\t" /* t = a - Kb mod p - e */ \
+  "v_add_u32 %1, %0, %16\n\t"                                        \
+  "v_min_u32 %0, %0, %1\n\t" /* kk = (a - Kb - e) mod p */
+#define DSE_PLANE_MARK(PB)               \
+  "v_and_or_b32 %1, %0, %17, " PB "\n\t" \
+  "v_lshlrev_b32 %2, %0, %18\n\t"        \
+  "ds_or_b32 %1, %2 offset:" DSE_IMG_OFF_S "\n\t"
+#define DSE_PLANE_NEXT "v_add_u32 %0, %0, %16\n\t"
 template <int NM>
 __device__ __forceinline__ void start_marks4(const uint32_t* a, const uint32_t* ne, const uint32_t* pb, uint32_t nKbm,
                                              uint32_t p, uint32_t one) {
   uint32_t t, u, b;
-  uint64_t sv;
   if (NM == 1)
     asm volatile(
-        "s_mov_b64 %3, exec\n\t"
-        "v_add3_u32 %0, %4, %16, %8\n\t"
-        "v_add_u32 %1, %0, %17\n\t"
-        "v_min_u32 %0, %0, %1\n\t"
-        "v_and_or_b32 %1, %0, %19, %12\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %3\n\t"
-        "v_add3_u32 %0, %5, %16, %9\n\t"
-        "v_add_u32 %1, %0, %17\n\t"
-        "v_min_u32 %0, %0, %1\n\t"
-        "v_and_or_b32 %1, %0, %19, %13\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %3\n\t"
-        "v_add3_u32 %0, %6, %16, %10\n\t"
-        "v_add_u32 %1, %0, %17\n\t"
-        "v_min_u32 %0, %0, %1\n\t"
-        "v_and_or_b32 %1, %0, %19, %14\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %3\n\t"
-        "v_add3_u32 %0, %7, %16, %11\n\t"
-        "v_add_u32 %1, %0, %17\n\t"
-        "v_min_u32 %0, %0, %1\n\t"
-        "v_and_or_b32 %1, %0, %19, %15\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %3"
-        : "=&v"(t), "=&v"(u), "=&v"(b), "=&s"(sv)
+        DSE_PLANE_START("%3", "%7") DSE_PLANE_MARK("%11")
+        DSE_PLANE_START("%4", "%8") DSE_PLANE_MARK("%12")
+        DSE_PLANE_START("%5", "%9") DSE_PLANE_MARK("%13")
+        DSE_PLANE_START("%6", "%10") DSE_PLANE_MARK("%14")
+        : "=&v"(t), "=&v"(u), "=&v"(b)
         : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(ne[0]), "v"(ne[1]), "v"(ne[2]), "v"(ne[3]), "v"(pb[0]),
-          "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(nKbm), "v"(p), "s"(KP), "s"(kBlockMask), "v"(one)
-        : "memory", "vcc");
-  else if (NM == 2)
+          "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(nKbm), "v"(p), "s"(kBlockMask), "v"(one)
+        : "memory");
+  else
     asm volatile(
-        "s_mov_b64 %3, exec\n\t"
-        "v_add3_u32 %0, %4, %16, %8\n\t"
-        "v_add_u32 %1, %0, %17\n\t"
-        "v_min_u32 %0, %0, %1\n\t"
-        "v_and_or_b32 %1, %0, %19, %12\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "v_add_u32 %0, %0, %17\n\t"
-        "v_and_or_b32 %1, %0, %19, %12\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %3\n\t"
-        "v_add3_u32 %0, %5, %16, %9\n\t"
-        "v_add_u32 %1, %0, %17\n\t"
-        "v_min_u32 %0, %0, %1\n\t"
-        "v_and_or_b32 %1, %0, %19, %13\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "v_add_u32 %0, %0, %17\n\t"
-        "v_and_or_b32 %1, %0, %19, %13\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %3\n\t"
-        "v_add3_u32 %0, %6, %16, %10\n\t"
-        "v_add_u32 %1, %0, %17\n\t"
-        "v_min_u32 %0, %0, %1\n\t"
-        "v_and_or_b32 %1, %0, %19, %14\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "v_add_u32 %0, %0, %17\n\t"
-        "v_and_or_b32 %1, %0, %19, %14\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %3\n\t"
-        "v_add3_u32 %0, %7, %16, %11\n\t"
-        "v_add_u32 %1, %0, %17\n\t"
-        "v_min_u32 %0, %0, %1\n\t"
-        "v_and_or_b32 %1, %0, %19, %15\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "v_add_u32 %0, %0, %17\n\t"
-        "v_and_or_b32 %1, %0, %19, %15\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %3"
-        : "=&v"(t), "=&v"(u), "=&v"(b), "=&s"(sv)
+        DSE_PLANE_START("%3", "%7") DSE_PLANE_MARK("%11") DSE_PLANE_NEXT DSE_PLANE_MARK("%11")
+        DSE_PLANE_START("%4", "%8") DSE_PLANE_MARK("%12") DSE_PLANE_NEXT DSE_PLANE_MARK("%12")
+        DSE_PLANE_START("%5", "%9") DSE_PLANE_MARK("%13") DSE_PLANE_NEXT DSE_PLANE_MARK("%13")
+        DSE_PLANE_START("%6", "%10") DSE_PLANE_MARK("%14") DSE_PLANE_NEXT DSE_PLANE_MARK("%14")
+        : "=&v"(t), "=&v"(u), "=&v"(b)
         : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(ne[0]), "v"(ne[1]), "v"(ne[2]), "v"(ne[3]), "v"(pb[0]),
-          "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(nKbm), "v"(p), "s"(KP), "s"(kBlockMask), "v"(one)
-        : "memory", "vcc");
-  else  // NM == 3: two marks, the first unconditional (every lane has kk < p <= pmax < KP)
-    asm volatile(
-        "s_mov_b64 %3, exec\n\t"
-        "v_add3_u32 %0, %4, %16, %8\n\t"
-        "v_add_u32 %1, %0, %17\n\t"
-        "v_min_u32 %0, %0, %1\n\t"
-        "v_and_or_b32 %1, %0, %19, %12\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "v_add_u32 %0, %0, %17\n\t"
-        "v_and_or_b32 %1, %0, %19, %12\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %3\n\t"
-        "v_add3_u32 %0, %5, %16, %9\n\t"
-        "v_add_u32 %1, %0, %17\n\t"
-        "v_min_u32 %0, %0, %1\n\t"
-        "v_and_or_b32 %1, %0, %19, %13\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "v_add_u32 %0, %0, %17\n\t"
-        "v_and_or_b32 %1, %0, %19, %13\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %3\n\t"
-        "v_add3_u32 %0, %6, %16, %10\n\t"
-        "v_add_u32 %1, %0, %17\n\t"
-        "v_min_u32 %0, %0, %1\n\t"
-        "v_and_or_b32 %1, %0, %19, %14\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "v_add_u32 %0, %0, %17\n\t"
-        "v_and_or_b32 %1, %0, %19, %14\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %3\n\t"
-        "v_add3_u32 %0, %7, %16, %11\n\t"
-        "v_add_u32 %1, %0, %17\n\t"
-        "v_min_u32 %0, %0, %1\n\t"
-        "v_and_or_b32 %1, %0, %19, %15\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "v_add_u32 %0, %0, %17\n\t"
-        "v_and_or_b32 %1, %0, %19, %15\n\t"
-        "v_lshlrev_b32 %2, %0, %20\n\t"
-        "v_cmpx_gt_u32_e32 vcc, %18, %0\n\t"
-        "ds_or_b32 %1, %2\n\t"
-        "s_mov_b64 exec, %3"
-        : "=&v"(t), "=&v"(u), "=&v"(b), "=&s"(sv)
-        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(ne[0]), "v"(ne[1]), "v"(ne[2]), "v"(ne[3]), "v"(pb[0]),
-          "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(nKbm), "v"(p), "s"(KP), "s"(kBlockMask), "v"(one)
-        : "memory", "vcc");
+          "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(nKbm), "v"(p), "s"(kBlockMask), "v"(one)
+        : "memory");
 }
 
-// MODE 0 with TT = 1..4: at most TT hits per plane after the n_min run
-// (mark_tail_n); TT = 0: the loop.
-template <int MODE, int TT = 0>
+// MODE 0: n_run marks per plane (TAIL false: n_min + the tail, the ones past
+// the segment dropped), or n_run = n_min marks and a loop for the rest (TAIL
+// true: sets whose primes spread over a wide range of hit counts).
+template <int MODE, bool TAIL = false>
 __device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, const PlaneSteps& ps,
-                                            uint32_t n_min) {
+                                            uint32_t n_run) {
   const uint32_t p = o.p;
   if (MODE != 0) {
-    constexpr int NM = MODE == 2 ? 1 : MODE == 1 ? 2 : 3;  // MODE 3: MODE 1 with pmax < KP
+    constexpr int NM = MODE == 2 ? 1 : 2;  // marks per plane
     start_marks4<NM>(o.a, ps.ne, ps.pb, nKbm, p, ps.one);
     start_marks4<NM>(o.a + 4, ps.ne + 4, ps.pb + 4, nKbm, p, ps.one);
     return;
   }
 #pragma unroll
   for (uint32_t q = 0; q < 8; ++q) {
-    uint32_t kk = plane_start(o.a[q], nKbm, ps.ne[q], p);
+    const uint32_t kk = plane_start(o.a[q], nKbm, ps.ne[q], p);
     const uint32_t pb4 = ps.pb[q];
-    kk = mark_run(pb4, kk, p, n_min, ps.one);
-    if (TT == 0) mark_tail(pb4, kk, p, ps.one);
-    else mark_tail_n<TT>(pb4, kk, p, ps.one);
+    const uint32_t k = mark_run(pb4, kk, p, n_run, ps.one);
+    if (TAIL) mark_tail(pb4, k, p, ps.one);
   }
 }
 
@@ -1040,18 +853,14 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
   const uint32_t n_min = (none || pmax >= KP) ? 0u : div_small(KP, pmax, fast_rcp((float)pmax));
   if (!none) {  // every lane live and past p^2: branch-free bodies
     if (pmin > KP) unit_L_fast<2>(o, nKbm, ps, 0);
-    else if (pmin > KP / 2 && pmax < KP) unit_L_fast<3>(o, nKbm, ps, 0);
     else if (pmin > KP / 2) unit_L_fast<1>(o, nKbm, ps, 0);
     else {
       // a lane has at most ceil(KP / p) <= ceil(KP / pmin) hits per plane, so
       // at most n_tail after the run
       const uint32_t n_tail =
           (uint32_t)__builtin_amdgcn_readfirstlane(div_ceil_small(KP, pmin, fast_rcp((float)pmin))) - n_min;
-      if (pmax < KP && n_tail == 1) unit_L_fast<0, 1>(o, nKbm, ps, n_min);
-      else if (pmax < KP && n_tail == 2) unit_L_fast<0, 2>(o, nKbm, ps, n_min);
-      else if (pmax < KP && n_tail == 3) unit_L_fast<0, 3>(o, nKbm, ps, n_min);
-      else if (pmax < KP && n_tail == 4) unit_L_fast<0, 4>(o, nKbm, ps, n_min);
-      else unit_L_fast<0>(o, nKbm, ps, n_min);
+      if (n_tail <= kShortTail) unit_L_fast<0>(o, nKbm, ps, n_min + n_tail);
+      else unit_L_fast<0, true>(o, nKbm, ps, n_min);
     }
     return;
   }
@@ -1060,7 +869,7 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
   const bool slow = p2 > Vs;
   const uint32_t D = slow && live ? (uint32_t)(p2 - Vs) : 0u;
   if (!live) return;
-  // Primes above KP/2 mark branch-free: two predicated marks (mark_plane<true>).
+  // Primes above KP/2 mark branch-free: two marks, dropped past the segment.
 #pragma unroll
   for (uint32_t q = 0; q < 8; ++q) {
     uint32_t kk = plane_start(o.a[q], nKbm, ps.ne[q], p);
@@ -1078,10 +887,10 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
     }
     const uint32_t pb4 = ps.pb[q];
     if (pmin > KP / 2) {
-      mark_plane<true>(pb4, kk, ps.one);
-      mark_plane<true>(pb4, kk + p, ps.one);
+      mark_k(pb4, kk, ps.one);
+      mark_k(pb4, kk + p, ps.one);
     } else {
-      for (; kk < KP; kk += p) mark_plane<false>(pb4, kk, ps.one);
+      for (; kk < KP; kk += p) mark_k(pb4, kk, ps.one);
     }
   }
 }
@@ -1095,8 +904,7 @@ constexpr uint32_t kBkGrid0 = DSE_BK_GRID;                         // band-0 col
 constexpr uint32_t kBk0Lists = DSE_BK0_LISTS;                      // band-0 columns per bucket unit
 static_assert(kBkGrid0 % kBk0Lists == 0 && 64 % kBk0Lists == 0, "band-0 bucket units");
 
-struct WheelLds {
-  uint32_t img[IMG_WORDS];         // the segment image, at LDS address 0
+struct WheelLdsLow {
   uint64_t mid_m[kMidCap];         // Barrett factors of the staged mid primes
   uint32_t mid_p[kMidCap];         // p | (30^{-1} mod p) << 16
   uint32_t mid_x[kMidCap];         // Vs mod p of this workgroup's segment (MidRes)
@@ -1108,15 +916,20 @@ struct WheelLds {
   uint32_t ctr;                    // unit counter
   unsigned long long rcnt[kMaxRanges];  // per range: primes counted by this workgroup
 };
+static_assert(sizeof(WheelLdsLow) <= kImgOff, "LDS below the image");
+struct WheelLds : WheelLdsLow {
+  uint8_t pad[kImgOff - sizeof(WheelLdsLow)];
+  uint32_t img[IMG_WORDS];         // the segment image, at LDS byte kImgOff, the top of the allocation
+};
+static_assert(sizeof(WheelLds) == kImgOff + IMG_BYTES, "the image ends the allocation");
 
 // BK: the range has bucketed primes (wa.bk_*). Two instantiations, so the
 // ranges without (N up to 1.1e12) run a unit loop without the bucket code
 // (with it, the loop's SGPR spills doubled and 1e11 ran 1.9% slower).
 template <bool BK>
 __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restrict__ table, WheelArgs wa) {
-  // One static LDS object, so the image sits at LDS address 0 (mark_k and
-  // a_classes combine a block's byte address and a plane with a bitwise or,
-  // and bound it by IMG_BYTES).
+  // One static LDS object at LDS address 0, so the image sits at kImgOff,
+  // the value every mark's ds_or adds in its offset field.
   __shared__ WheelLds lds;
   uint64_t* const s_mid_m = lds.mid_m;
   uint32_t* const s_mid_p = lds.mid_p;
@@ -1384,7 +1197,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     // hoists dozens of them out of the round loop and spills them. Recompute.
     uint32_t lane = lane_id;
     asm volatile("" : "+v"(lane));
-    const uint32_t img0 = lds_addr(img);
+    const uint32_t img0 = lds_addr(img) - kImgOff;  // 0: mark addresses are image-relative
     const uint32_t one = opaque(1u);
     // Bucketed hits of the primes > kWheelMaxPrime as units of the queue,
     // interleaved with the marking units, so their global-load latency
