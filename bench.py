@@ -164,6 +164,32 @@ def pmc_summary(N: int, P: int, window: bool):
     return None
 
 
+def pmc_window_traffic():
+    """HBM bytes of one --window sieve call from the newest committed PMC passes
+    (profiles/<round>/pmc_window_{fetch,write}.csv: rocprofv3 --pmc FETCH_SIZE /
+    WRITE_SIZE of `bench.py --window`): 2*FETCH_SIZE + WRITE_SIZE (KiB counters,
+    MI355X_MICROARCH.md gfx950 correction) summed over every kernel, divided by
+    the wheel-kernel dispatches (one per call)."""
+    import csv
+    import glob
+    for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")), reverse=True):
+        try:
+            tot = {}
+            for c, f in (("FETCH_SIZE", "pmc_window_fetch.csv"), ("WRITE_SIZE", "pmc_window_write.csv")):
+                rows = list(csv.DictReader(open(os.path.join(d, f))))
+                calls = {r["Dispatch_Id"] for r in rows if "wheel_segments_kernel" in r["Kernel_Name"]}
+                tot[c] = sum(float(r["Counter_Value"]) for r in rows if r["Counter_Name"] == c) / len(calls)
+            try:
+                build = json.load(open(os.path.join(d, "pmc_build.json")))
+            except OSError:
+                build = None
+            return {"traffic": (2 * tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) * 1024, "source": os.path.relpath(d, ROOT),
+                    "build": build}
+        except (OSError, KeyError, ZeroDivisionError):
+            continue
+    return None
+
+
 def lds_instr_check(wm: int, cs: int, pmc):
     """The analytic executed-mark count against the PMC's LDS wave-instructions
     per launch: SQ_INSTS_LDS = the marks (wm / 64 full-wave ds_or_b32) + the
@@ -391,6 +417,28 @@ def run(a, world: int, rank: int, wd: Watchdog):
         if a.window:
             workload = f"window [1e18, 1e18+1e10] split into {P} slice(s), one per GPU (count only, segment-only)"
             rf = None
+            # the bucketed pass is the window's dominant cost (bucket fill/stage
+            # ~57% of a call): HBM-bound on its entries, 4 B written by the fill
+            # and read back by the wheel kernel per hit of a prime > 2^19
+            entries = work.WINDOW_BUCKET_ENTRIES * cs / nb_all  # this rank's share (exact at one rank)
+            alg = 2 * work.BUCKET_ENTRY_BYTES * entries
+            wp = pmc_window_traffic()
+            achieved = alg / ks / 1e9
+            window_roofline = {
+                "bound": "hbm", "achieved": achieved, "peak": work.HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / work.HBM_PEAK_GBS,
+                "traffic": wp["traffic"] * cs / nb_all if wp else None,
+                "traffic_source": f"committed PMC passes {wp['source']} (not this run; scaled to this rank's share)"
+                                  if wp else None,
+                "kernel": "the window's bucketed sieve call: every kernel of one sieve_range call (bucket range, "
+                          "count, column/start scans, fill + stage, sort, wheel kernel), HIP events on its stream",
+                "kernel_ms": ks * 1e3,
+                "bucket_entries_per_launch": entries,
+                "basis": "8 B per bucket entry (4 B written by bucket_fill_stage_kernel / the band-1 sort, 4 B read "
+                         "back by the wheel kernel) of every hit p*m, gcd(m, 30) = 1, of the primes 2^19 < p <= 1e9+4 "
+                         "in the window (mail_sieve_e/work.py WINDOW_BUCKET_ENTRIES, tools/window_entries.py) against "
+                         "8 TB/s HBM",
+            }
         else:
             workload = (f"N={N:.0e} odd-only chunked sieve, P={P} spread-work chunks (one per GPU), mask resident "
                         "in HBM" + (" [count-only diagnostic]" if a.no_mask else ""))
@@ -423,6 +471,8 @@ def run(a, world: int, rank: int, wd: Watchdog):
             "cpu_baseline": None,
             "world": world_info,
         }
+        if a.window:
+            out["roofline"] = window_roofline
         if rf is not None:
             wm = rf["wheel_marks"]
             achieved = work.LDS_OR_BYTES_PER_MARK * wm / ks / 1e9

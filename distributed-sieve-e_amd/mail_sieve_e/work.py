@@ -96,6 +96,38 @@ def wheel_marks_for_range(g_start: int, nbits: int) -> int:
     return int(cnt.sum())
 
 
+BUCKET_LO = 2**19  # ranges with bucketed primes bucket every prime above this (csrc kBucketLoLog)
+
+
+def bucket_entries_for_range(g_start: int, nbits: int, lo_p: int = BUCKET_LO) -> int:
+    """Bucket entries the bucketed pass writes (and the wheel kernel reads
+    back) for the odd-index range: one per multiple p*m in the range with
+    gcd(m, 30) = 1 and p*m >= p^2 of every prime lo_p < p <= sqrt(vmax)
+    (csrc/dse_wheel.hip bucket_fill_stage_kernel; the range must reach past
+    2^20, or the wheel kernel takes all its primes itself). Needs the primes up
+    to sqrt(vmax): ~0.5 GB and ~10 s of numpy for the 1e18 window
+    (tools/window_entries.py keeps that one as WINDOW_BUCKET_ENTRIES)."""
+    if nbits <= 0:
+        return 0
+    va = 3 + 2 * g_start
+    vb = 3 + 2 * (g_start + nbits - 1)
+    ps = odd_primes_upto(math.isqrt(vb))
+    ps = ps[ps > lo_p]
+    if ps.size == 0:
+        return 0
+    lo = np.maximum(ps * ps, va)
+    m0 = (lo + ps - 1) // ps
+    m1 = vb // ps
+    cnt = np.where(m1 >= m0, _coprime30_upto(m1) - _coprime30_upto(m0 - 1), 0)
+    return int(cnt.sum())
+
+
+# bucket_entries_for_range of bench.py --window's range (odd values 1e18 + 1 ..
+# 1e18 + 1e10 - 1; tools/window_entries.py): 8 B each is written and read back
+WINDOW_BUCKET_ENTRIES = 1_208_549_165
+BUCKET_ENTRY_BYTES = 4
+
+
 def roofline(g_start: int, nbits: int, seconds: float, launches: int = 1) -> dict:
     """t_roof = max(8*marks/BW_LDS, (nbits/8)/BW_HBM), marks =
     the algorithmic odd-only count. The wheel kernel issues fewer LDS marks

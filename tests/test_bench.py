@@ -77,10 +77,28 @@ def test_bench_window_two_rank_rehearsal():
     d = _last_json(r.stdout)
     assert d["n_gpus"] == 2 and d["verified"] is True and d["pi_full"] == 241272176
     assert d["config"]["P"] == 2 and d["value"] > 0
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and 0 < rf["frac"] <= 1 and abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-9
     # the window's 203 MB of primes are not broadcast: every rank builds its table
     t = d["world"]["base_table"]
     assert t["path"] == "local" and t["bytes"] > 8 << 20
     assert [x["rank"] for x in d["world"]["ranks"]] == [0, 1] and all(x["kernel_ms"] > 0 for x in d["world"]["ranks"])
+
+
+@pytest.mark.gpu
+def test_bench_window_single_gpu_line():
+    """BASELINE config 5 on one GPU: the count verified and an HBM roofline of
+    the bucketed pass (8 B per bucket entry, WINDOW_BUCKET_ENTRIES of them)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--window", "--steps", "3", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _last_json(r.stdout)
+    assert d["verified"] is True and d["pi_full"] == 241272176 and d["n_gpus"] == 1
+    rf = d["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and 0 < rf["frac"] <= 1
+    assert abs(rf["achieved"] - 8 * 1_208_549_165 / (rf["kernel_ms"] / 1e3) / 1e9) < 1e-6 * rf["achieved"]
+    # one rank: nothing to share, the table is built where it is used
+    assert d["world"]["base_table"]["path"] == "local"
 
 
 @pytest.mark.gpu

@@ -11,4 +11,5 @@ tail -12 $OUT/configs.log
 for np in "1e10 2" "1e10 4" "1e10 8" "1e11 2" "1e11 4" "1e11 8" "1e12 8"; do
   timeout -k 10 240 python tools/rank_steps.py $np >> $OUT/rank_steps.txt 2>&1 || { tail -20 $OUT/rank_steps.txt; exit 1; }
 done
-grep -E "critical|^N=" $OUT/rank_steps.txt
+timeout -k 10 240 python tools/rank_steps.py window 8 >> $OUT/rank_steps.txt 2>&1 || { tail -20 $OUT/rank_steps.txt; exit 1; }
+grep -E "critical|^N=|^window" $OUT/rank_steps.txt
