@@ -14,6 +14,9 @@ namespace dse {
 //   [align32(..), +32cap) uint32 a[8cap] wheel offsets, row i rotated by i mod 8:
 //                                        a[8i+j] = first k >= 0 with p | R30[(j+i)&7] + 30k
 //                                        (p >= 7; 0 for p = 3, 5)
+//   [align32(..)+32cap, +8cap) uint32 pl[2][cap] the wheel kernel's large-prime words: p | plan << 20,
+//                                        plan = the marking plan of the prime's set of 64 (unit_L;
+//                                        pl[0] for 2^17-period segments, pl[1] for 2^16)
 struct TableHeader {
   uint32_t count;
   uint32_t cap;
@@ -26,8 +29,9 @@ __host__ __device__ inline uint64_t table_m_offset(uint32_t cap) {
 __host__ __device__ inline uint64_t table_a_offset(uint32_t cap) {
   return (table_m_offset(cap) + 8ull * cap + 31ull) & ~31ull;
 }
+__host__ __device__ inline uint64_t table_l_offset(uint32_t cap) { return table_a_offset(cap) + 32ull * cap; }
 __host__ __device__ inline uint64_t table_bytes_for_cap(uint32_t cap) {
-  return table_a_offset(cap) + 32ull * cap;
+  return table_l_offset(cap) + 8ull * cap;
 }
 
 // The 8 residues mod 30 coprime to 30 (wheel planes, absolute numbering).
@@ -46,7 +50,10 @@ constexpr uint64_t kWheelOutBits = kWheelSpan / 2;      // odd candidates per se
 // Ranges with base primes above this go through the bucketed pass
 // (dse_wheel.hip), which then buckets every prime above 2^kBucketLoLog.
 #ifndef DSE_WHEEL_MAX_LOG
-#define DSE_WHEEL_MAX_LOG 20  // A/B builds only (r05 window: 2^22 7.25 ms, 2^21 6.11, 2^20 5.62, 2^19 5.49)
+// Builds support 19 and 20 only: the L list's table words carry the prime in
+// 20 bits (dse_wheel.hip kLPrimeMask), and the bucket threshold 2^19 must not
+// exceed it. (r05 window A/B: 2^22 7.25 ms, 2^21 6.11, 2^20 5.62, 2^19 5.49)
+#define DSE_WHEEL_MAX_LOG 20
 #endif
 constexpr uint64_t kWheelMaxPrime = 1ull << DSE_WHEEL_MAX_LOG;
 

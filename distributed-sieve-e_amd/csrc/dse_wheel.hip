@@ -25,7 +25,7 @@
 // One workgroup of 1024 threads per CU, segments blockIdx.x + t*gridDim.x.
 // Per segment:
 //   1. mark (ds_or_b32), units taken from one LDS counter:
-//      A  (61 < p <= TA): one prime per wave; lane (plane i, c = 0..7) takes
+//      A  (79 < p <= TA): one prime per wave; lane (plane i, c = 0..7) takes
 //         the hits n of its plane with n mod 256 in [32c, 32c+32), by class
 //         n mod 256: a class's hits sit 256p periods apart, same bit, so each
 //         further mark is one v_add; the 4 lanes of a plane in a half-wave
@@ -40,7 +40,7 @@
 //   2. expand: lane reads one block (two ds_read_b128), transposes the 8x32
 //      bits into 32 period bytes, maps each through a 256-entry LDS table to
 //      the 15 odd slots of its period (composite bits in, prime slots out),
-//      packs 480 output bits, fixes the small primes 3..61, masks the range
+//      packs 480 output bits, fixes the small primes 3..79, masks the range
 //      end, popcounts, stores; then each wave inits (patterns of 7..61) the
 //      blocks it expanded, for the next segment.
 // See DESIGN.md section 4 for the rooflines.
@@ -72,6 +72,8 @@ static_assert(IMG_BYTES == KP, "a period index is its block's byte address");
 // end are issued unconditionally, without a compare and exec masking.
 #define DSE_IMG_OFF_S "32768"
 constexpr uint32_t kImgOff = 32768;
+#define DSE_STR2(x) #x
+#define DSE_STR(x) DSE_STR2(x)
 constexpr uint32_t NT = 1024;
 constexpr uint32_t NW = NT / 64;            // waves; every wave marks, expands and inits
 static_assert(BLOCKS % (64 * NW) == 0, "expansion blocks");
@@ -93,7 +95,7 @@ static_assert(BLOCKS % (64 * NW) == 0, "expansion blocks");
 #endif
 constexpr uint32_t TA = DSE_TA;             // A/B1 threshold
 #ifndef DSE_TB1
-#define DSE_TB1 384
+#define DSE_TB1 512
 #endif
 constexpr uint32_t TB1 = DSE_TB1;           // B1/B2 threshold
 #ifndef DSE_TB
@@ -102,7 +104,7 @@ constexpr uint32_t TB1 = DSE_TB1;           // B1/B2 threshold
 constexpr uint32_t TB = DSE_TB;             // B2/L threshold
 static_assert(TA <= 256 && TA < TB1 && TB1 <= TB && TB <= KP / 8, "unit thresholds");
 static_assert(KP / (128 * (TA + 1)) <= 10 && KP / (32 * (TB1 + 1)) <= 10, "class_marks_k covers K <= 10");
-constexpr uint32_t kMidCap = TB >= 16384 ? 1920 : TB >= 8192 ? 1040 : TB >= 4096 ? 580 : 320;  // odd primes in (61, TB]
+constexpr uint32_t kMidCap = TB >= 16384 ? 1920 : TB >= 8192 ? 1040 : TB >= 4096 ? 580 : 320;  // >= odd primes in (61, TB]
 constexpr uint32_t kOutWordsPerSeg = (uint32_t)(kWheelOutBits / 32);  // 30720
 
 constexpr uint32_t kQMax = 79;  // the pattern primes are 7..79
@@ -201,8 +203,8 @@ struct WheelArgs {
   WheelRange r[kMaxRanges];
   uint32_t nranges;    // 1..kMaxRanges (1 with bucketed primes)
   uint32_t nseg;       // segments of all ranges
-  uint32_t nthr[5];    // odd primes <= 61, TA, TB1, TB, kWheelMaxPrime (table indices of the unit lists)
-  // Bucketed hits of the primes > kWheelMaxPrime (bk_start null: none), as
+  uint32_t nthr[5];    // odd primes <= kQMax (79), TA, TB1, TB, kWheelMaxPrime (table indices of the unit lists)
+  // Bucketed hits of the primes > 2^kBucketLoLog, or the bucket_lo_log2 option (bk_start null: none), as
   // entries (bucket_entry):
   const uint32_t* bk_entries;  // band 1: segment s owns [bk_start[s], bk_start[s+1])
   const uint32_t* bk_start;
@@ -214,6 +216,10 @@ struct WheelArgs {
   uint32_t bk_k0;              // band-0 region capacity (0: no band 0 in the pass)
 };
 static_assert(sizeof(WheelArgs) <= 4096, "kernel arguments");
+// wheel_segments_kernel(table, wa): wa follows the 8-byte table pointer in the
+// kernel-argument segment
+constexpr uint32_t kWaOffset = 8;
+static_assert(alignof(WheelArgs) <= 8, "kernel argument layout");
 
 // 32-bit LDS byte address of a __shared__ pointer.
 __device__ __forceinline__ uint32_t lds_addr(const uint32_t* p) {
@@ -240,6 +246,39 @@ constexpr uint32_t kBlockMask = ~31u;  // period index -> its block's byte addre
 // MODE-0 L sets whose tail after the n_min run is at most this many steps mark
 // it unconditionally (past the segment: dropped) instead of in mark_tail's loop
 constexpr uint32_t kShortTail = DSE_SHORT_TAIL;
+// Odd primes <= TB: the table index where the L list (and its sets of 64
+// primes) starts whenever the table reaches past TB.
+constexpr uint32_t odd_primes_upto(uint32_t x) {
+  uint32_t c = 0;
+  for (uint32_t v = 3; v <= x; v += 2) {
+    bool pr = true;
+    for (uint32_t d = 3; d * d <= v; d += 2)
+      if (v % d == 0) { pr = false; break; }
+    c += pr;
+  }
+  return c;
+}
+constexpr uint32_t kL0 = odd_primes_upto(TB);
+// The marking plan of a set of 64 large primes pmin..pmax (unit_L), fixed by
+// the primes and the segment geometry, so the table carries it (pl[] words
+// p | plan << 20, wheel_offsets_kernel) instead of each set deriving it per
+// segment with two divisions (~40 instructions): bits 0-1 MODE (2: pmin > KP,
+// one mark per plane; 1: pmin > KP/2, two; 0: runs), bit 2 a tail loop
+// follows the run, bits 3.. the run length: ceil(KP / pmin) (every lane's hit
+// count is at most that; the marks past the segment are dropped), or
+// floor(KP / pmax) (every lane's minimum) when the two differ by more than
+// kShortTail.
+constexpr uint32_t kLPrimeMask = 0x800FFFFFu;  // pl[] word -> p (bit 31: lane past the table end)
+static_assert(kWheelMaxPrime <= (1u << 20), "pl[] words: the L primes (odd, <= kWheelMaxPrime) are below 2^20");
+__host__ __device__ constexpr uint32_t l_plan(uint32_t pmin, uint32_t pmax, uint32_t kp) {
+  if (pmin > kp) return 2;
+  if (pmin > kp / 2) return 1;
+  const uint32_t n_min = pmax >= kp ? 0u : kp / pmax;
+  const uint32_t n_all = (kp + pmin - 1) / pmin;
+  return n_all - n_min <= kShortTail ? n_all << 3 : 4u | n_min << 3;
+}
+static_assert(l_plan(TB + 2, TB + 2, 1u << 17) < (1u << 12), "the plan fits 12 bits");
+static_assert(odd_primes_upto(kQMax) + kMidCap >= kL0, "the L list starts at kL0 whenever it exists");
 
 // Mark period k (< KP) of the plane whose byte base is pb4 (image + 4 plane):
 // address (k & ~31) | pb4 in one v_and_or, bit 1 << (k & 31) (the shift reads
@@ -542,7 +581,7 @@ __device__ __forceinline__ uint32_t mid_residue(const MidRes& mr, uint32_t i, ui
   return xs;
 }
 
-// A: one mid prime (61 < p <= TA) per wave; lane (plane L & 7, c = L >> 3).
+// A: one mid prime (kQMax < p <= TA) per wave; lane (plane L & 7, c = L >> 3).
 // Lanes 0-31 have c = 0..3: a plane's four lanes mark 32p periods apart at
 // every step (same class r, same t), i.e. in blocks c p (mod 4) apart -- four
 // distinct banks for odd p.
@@ -558,7 +597,7 @@ __device__ __forceinline__ void unit_A(uint32_t img0, uint32_t pi, uint64_t m, c
   const uint32_t pb4 = img0 + 4 * pl;
   const uint32_t k = kp + 32 * c * p;                   // class 0 of the lane: hit n = 32c
   if (p2 <= Vs) {
-    switch (KP / (256 * p)) {  // K (wave-uniform): 2..7 for 61 < p <= 256 (1..4 for the half geometry)
+    switch (KP / (256 * p)) {  // K (wave-uniform): 2..6 for kQMax < p <= TA (1..3 for the half geometry)
       case 1: a_classes<1>(pb4, k, p, one); return;
       case 2: a_classes<2>(pb4, k, p, one); return;
       case 3: a_classes<3>(pb4, k, p, one); return;
@@ -679,12 +718,23 @@ struct LargeOps {
 __device__ __forceinline__ void load_L(LargeOps& o, const uint32_t* __restrict__ P, const uint64_t* __restrict__ M,
                                        const uint32_t* __restrict__ A, uint32_t il, uint32_t np, bool need_m) {
   const uint32_t ic = min(il, np - 1);  // past the table end: load the last row, mark nothing
-  o.p = il < np ? P[ic] : 0x7FFFFFFFu;
+  // p | plan << 20 (table pl[]); past the table end bit 31 marks the lane dead
+  // (a load under exec into the preset register: a select after an
+  // unconditional load would wait for the load right here)
+  o.p = il < np ? *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(P) + (ic << 2)) : 0xFFFFFFFFu;
   o.m = need_m ? M[ic] : 0ull;  // the Barrett factor: only for Kb >= 2^38 (unit_L); 1e12: -1.9%
-  const uint4* row = reinterpret_cast<const uint4*>(A + 8ull * ic);
+  // 32-bit byte offset from the table's base (one VALU, no 64-bit address math)
+  const uint4* row = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(A) + (ic << 5));
   const uint4 lo = row[0], hi = row[1];
   o.a[0] = lo.x; o.a[1] = lo.y; o.a[2] = lo.z; o.a[3] = lo.w;
   o.a[4] = hi.x; o.a[5] = hi.y; o.a[6] = hi.z; o.a[7] = hi.w;
+}
+
+// Operand registers whose contents are dead: left undefined (an empty asm
+// that "writes" them), so the compiler keeps no copy of what they held.
+__device__ __forceinline__ void undef_ops(LargeOps& o) {
+  asm volatile("" : "=v"(o.p), "=v"(o.m), "=v"(o.a[0]), "=v"(o.a[1]), "=v"(o.a[2]), "=v"(o.a[3]), "=v"(o.a[4]),
+               "=v"(o.a[5]), "=v"(o.a[6]), "=v"(o.a[7]));
 }
 
 // Mark a bucketed hit: entry = LDS word index << 5 | bit (bucket_entry), so
@@ -783,19 +833,55 @@ __device__ __forceinline__ void start_marks4(const uint32_t* a, const uint32_t* 
         : "memory");
 }
 
+#ifndef DSE_LOCKSTEP
+#define DSE_LOCKSTEP 1
+#endif
+// One mark in each of the 8 planes, k[q] += p: 32 instructions in one block
+// (two scratch pairs alternate, as in mark_k_step4, so a ds_or's operands are
+// not rewritten by the next instruction).
+#define DSE_MARK8_ONE(A, B, K, PB)                   \
+  "v_and_or_b32 " A ", " K ", %21, " PB "\n\t"     \
+  "v_lshlrev_b32 " B ", " K ", %22\n\t"             \
+  "v_add_u32 " K ", " K ", %20\n\t"                 \
+  "ds_or_b32 " A ", " B " offset:" DSE_IMG_OFF_S "\n\t"
+__device__ __forceinline__ void mark8(uint32_t (&k)[8], const uint32_t* pb, uint32_t p, uint32_t one) {
+  uint32_t a0, b0, a1, b1;
+  asm volatile(DSE_MARK8_ONE("%0", "%1", "%4", "%12") DSE_MARK8_ONE("%2", "%3", "%5", "%13")
+                   DSE_MARK8_ONE("%0", "%1", "%6", "%14") DSE_MARK8_ONE("%2", "%3", "%7", "%15")
+                       DSE_MARK8_ONE("%0", "%1", "%8", "%16") DSE_MARK8_ONE("%2", "%3", "%9", "%17")
+                           DSE_MARK8_ONE("%0", "%1", "%10", "%18") DSE_MARK8_ONE("%2", "%3", "%11", "%19")
+               : "=&v"(a0), "=&v"(b0), "=&v"(a1), "=&v"(b1), "+v"(k[0]), "+v"(k[1]), "+v"(k[2]), "+v"(k[3]),
+                 "+v"(k[4]), "+v"(k[5]), "+v"(k[6]), "+v"(k[7])
+               : "v"(pb[0]), "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(pb[4]), "v"(pb[5]), "v"(pb[6]), "v"(pb[7]),
+                 "v"(p), "s"(kBlockMask), "v"(one)
+               : "memory");
+}
+
 // MODE 0: n_run marks per plane (TAIL false: n_min + the tail, the ones past
 // the segment dropped), or n_run = n_min marks and a loop for the rest (TAIL
 // true: sets whose primes spread over a wide range of hit counts).
 template <int MODE, bool TAIL = false>
-__device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, const PlaneSteps& ps,
+__device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t p, uint32_t nKbm, const PlaneSteps& ps,
                                             uint32_t n_run) {
-  const uint32_t p = o.p;
   if (MODE != 0) {
     constexpr int NM = MODE == 2 ? 1 : 2;  // marks per plane
     start_marks4<NM>(o.a, ps.ne, ps.pb, nKbm, p, ps.one);
     start_marks4<NM>(o.a + 4, ps.ne + 4, ps.pb + 4, nKbm, p, ps.one);
     return;
   }
+#if DSE_LOCKSTEP
+  if (!TAIL) {
+    // all 8 planes in lockstep: one asm block marks hit h of every plane, so
+    // the loop control is paid once per 8 marks (the plane starts take the
+    // operand row's registers)
+    uint32_t kk[8];
+#pragma unroll
+    for (uint32_t q = 0; q < 8; ++q) kk[q] = plane_start(o.a[q], nKbm, ps.ne[q], p);
+#pragma unroll 1
+    for (uint32_t h = 0; h < n_run; ++h) mark8(kk, ps.pb, p, ps.one);
+    return;
+  }
+#endif
 #pragma unroll
   for (uint32_t q = 0; q < 8; ++q) {
     const uint32_t kk = plane_start(o.a[q], nKbm, ps.ne[q], p);
@@ -811,8 +897,9 @@ __device__ __forceinline__ void unit_L_fast(const LargeOps& o, uint32_t nKbm, co
 // operand registers)
 template <bool BARRETT>
 __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t Vend, uint64_t Kb,
-                                       const PlaneSteps& ps, uint32_t pl_rot, uint64_t rho_pack) {
-  const uint32_t p = o.p;
+                                       const PlaneSteps& ps, uint32_t pl_rot, const uint64_t* rho_pack_p,
+                                       uint32_t sqrt_vs) {
+  const uint32_t p = o.p & kLPrimeMask;  // the prime (>= 2^31: a lane past the table end)
   const float invp = fast_rcp((float)p);
   // Kb mod p. While Kb < 2^32 (values below 1.29e11; wave-uniform) a float
   // quotient is within one of the true one: its relative error is below
@@ -842,33 +929,31 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
     kbm = mod_barrett(Kb, p, o.m);
   }
   const uint32_t nKbm = 0u - kbm;
-  const uint32_t pmin = __builtin_amdgcn_readfirstlane(p);
   const uint32_t pmax = __builtin_amdgcn_readlane(p, 63);
   // some lane not live or with p^2 inside the segment: the set's primes
-  // ascend (lanes past the table end hold 0x7FFFFFFF), so pmax decides, on
+  // ascend (lanes past the table end hold 2^31 and up), so pmax decides, on
   // the scalar unit (a per-lane 64-bit p^2 and two compares: 1e12 +1.4%)
-  const bool none = (uint64_t)pmax * pmax > Vs;
-  // every plane start kk is below p <= pmax (plane_start), so each lane has at
-  // least floor(KP / pmax) hits per plane: kk + (n - 1) p <= p - 1 + KP - p
-  const uint32_t n_min = (none || pmax >= KP) ? 0u : div_small(KP, pmax, fast_rcp((float)pmax));
-  if (!none) {  // every lane live and past p^2: branch-free bodies
-    if (pmin > KP) unit_L_fast<2>(o, nKbm, ps, 0);
-    else if (pmin > KP / 2) unit_L_fast<1>(o, nKbm, ps, 0);
-    else {
-      // a lane has at most ceil(KP / p) <= ceil(KP / pmin) hits per plane, so
-      // at most n_tail after the run
-      const uint32_t n_tail =
-          (uint32_t)__builtin_amdgcn_readfirstlane(div_ceil_small(KP, pmin, fast_rcp((float)pmin))) - n_min;
-      if (n_tail <= kShortTail) unit_L_fast<0>(o, nKbm, ps, n_min + n_tail);
-      else unit_L_fast<0, true>(o, nKbm, ps, n_min);
-    }
+  const bool none = pmax > sqrt_vs;  // pmax^2 > Vs, sqrt_vs = isqrt(Vs)
+  if (!none) {  // every lane live and past p^2: branch-free bodies chosen by the set's plan
+    const uint32_t plan = (uint32_t)__builtin_amdgcn_readfirstlane(o.p) >> 20;  // lane 0: live
+    const uint32_t n_run = plan >> 3;
+    if ((plan & 3) == 2) unit_L_fast<2>(o, p, nKbm, ps, 0);
+    else if ((plan & 3) == 1) unit_L_fast<1>(o, p, nKbm, ps, 0);
+    else if (!(plan & 4)) unit_L_fast<0>(o, p, nKbm, ps, n_run);
+    else unit_L_fast<0, true>(o, p, nKbm, ps, n_run);
     return;
   }
+  const uint32_t pmin = __builtin_amdgcn_readfirstlane(p);
   const uint64_t p2 = (uint64_t)p * p;
   const bool live = p2 < Vend;
   const bool slow = p2 > Vs;
   const uint32_t D = slow && live ? (uint32_t)(p2 - Vs) : 0u;
   if (!live) return;
+  // read here, not passed in: the compiler rematerialises a kernel-argument
+  // value by a scalar load, and hoisted into the common path that load (with
+  // the s_waitcnt lgkmcnt(0) before its register is reused) drained every
+  // wave's outstanding marks once per set
+  const uint64_t rho_pack = *(volatile const uint64_t*)rho_pack_p;
   // Primes above KP/2 mark branch-free: two marks, dropped past the segment.
 #pragma unroll
   for (uint32_t q = 0; q < 8; ++q) {
@@ -942,11 +1027,19 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       reinterpret_cast<const uint64_t*>(reinterpret_cast<const char*>(table) + table_m_offset(th->cap));
   const uint32_t* __restrict__ A =
       reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + table_a_offset(th->cap));
+  // the L list's words p | plan << 20 for this geometry (table pl[0] / pl[1])
+  const uint32_t* __restrict__ PL = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) +
+                                                                    table_l_offset(th->cap)) +
+                                    (kWheelLogKP == 17 ? 0u : th->cap);
 
+#if defined(DSE_PAD_NOPS) && DSE_PAD_NOPS > 0
+  // code-placement A/B only: shifts the kernel's instruction stream by 4 B each
+  asm volatile(".rept " DSE_STR(DSE_PAD_NOPS) "\n\ts_nop 0\n\t.endr");
+#endif
   const uint32_t tid = threadIdx.x, lane_id = tid & 63, wave = tid >> 6;
 
   if (tid == 0) {
-    // first index with p > 61, > TA, > TB1, > TB (capped by the LDS stage),
+    // first index with p > kQMax, > TA, > TB1, > TB (capped by the LDS stage),
     // > kWheelMaxPrime (bucketed or absent): the table holds every odd prime
     // from 3 up, so these are the host's prime counts (wa.nthr), capped by
     // the table's size
@@ -1199,7 +1292,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     asm volatile("" : "+v"(lane));
     const uint32_t img0 = lds_addr(img) - kImgOff;  // 0: mark addresses are image-relative
     const uint32_t one = opaque(1u);
-    // Bucketed hits of the primes > kWheelMaxPrime as units of the queue,
+    // Bucketed hits of the primes > 2^kBucketLoLog as units of the queue,
     // interleaved with the marking units, so their global-load latency
     // overlaps other waves' marking instead of stalling every wave at the
     // segment start: n0u band-0 units (kBk0Lists columns each), then band-1
@@ -1213,6 +1306,20 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       n1u = (bk_b1 - bk_b0 + kBkUnit - 1) / kBkUnit;
       n3 = n0u + n1u + (wa.bk_k0 && *wa.bk_nspill ? 1u : 0u);
     }
+    // the range's rho_pack in the kernel-argument segment (after the table
+    // pointer), for unit_L's rare slow path: not &rg.rho_pack, which would
+    // make the compiler copy the whole argument block to scratch
+    const uint64_t* rho_pack_p = reinterpret_cast<const uint64_t*>(
+        (const char*)__builtin_amdgcn_kernarg_segment_ptr() + kWaOffset +
+        range_of(g_seg) * sizeof(WheelRange) + offsetof(WheelRange, rho_pack));
+    uint32_t sqrt_vs = (uint32_t)__builtin_sqrt((double)Vs);  // isqrt(Vs) < 2^32 (Vs < 2^64)
+    while ((uint64_t)sqrt_vs * sqrt_vs > Vs) --sqrt_vs;
+    while ((uint64_t)(sqrt_vs + 1) * (sqrt_vs + 1) <= Vs) ++sqrt_vs;
+    sqrt_vs = __builtin_amdgcn_readfirstlane(sqrt_vs);
+    uint32_t sqrt_ve = (uint32_t)__builtin_sqrt((double)(Vend - 1));  // p^2 < Vend <=> p <= isqrt(Vend - 1)
+    while ((uint64_t)sqrt_ve * sqrt_ve > Vend - 1) --sqrt_ve;
+    while ((uint64_t)(sqrt_ve + 1) * (sqrt_ve + 1) <= Vend - 1) ++sqrt_ve;
+    sqrt_ve = __builtin_amdgcn_readfirstlane(sqrt_ve);
     const uint32_t rot = (i_mid1 + lane) & 7;  // = table index & 7 of this lane's large primes
     // absolute residue (q + rot) & 7 at step q: its plane and e bit
     const uint32_t pl_rot = ((rg.pl_pack >> (3 * rot)) | (rg.pl_pack << (24 - 3 * rot))) & 0xFFFFFFu;
@@ -1263,27 +1370,53 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       return n3 > n_all ? ~0u : q - mb;
     };
     auto bk_of = [&](uint32_t q) -> uint32_t { return q < 2 * mb ? q >> 1 : q - mb; };
+    // a claimed queue position, decoded once: kind << 30 | index (kind 0: a mid
+    // unit of list 1, 1: a large unit, 2: a bucket unit), ~0u past the end
+    constexpr uint32_t kIdx = (1u << 30) - 1;
+    auto decode = [&](uint32_t q) -> uint32_t {
+      if (q >= n_q) return ~0u;
+      const uint32_t u = unit_of(q);
+      if (u == ~0u) return 2u << 30 | bk_of(q);
+      return (is_l(u) ? 1u << 30 : 0u) | idx_of(u);
+    };
+    // Operands are only ever loaded into nxt and copied to cur at the top of
+    // an iteration, after they have landed: had the first unit's loads gone
+    // straight into cur, the compiler's wait analysis, merging that entry
+    // with the loop's back edge, waited inside every unit for the next unit's
+    // loads just issued (a vmcnt(4) and a vmcnt(0) per large unit).
     LargeOps cur, nxt;
     LargeOps cur1, nxt1;  // the unit's second 64 primes
-    uint32_t q_cur = claimed(claim());
-    uint32_t q_nxt = claimed(claim());
-    if (q_cur < n_q && unit_of(q_cur) != ~0u && is_l(unit_of(q_cur))) {
-      load_L(cur, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_cur)) + lane, i_big, need_m);
-      load_L(cur1, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_cur)) + 64 + lane, i_big, need_m);
+    uint32_t d_nxt = decode(claimed(claim()));
+    if ((d_nxt >> 30) == 1) {
+      load_L(nxt, PL, M, A, i_mid1 + kLU * (d_nxt & kIdx) + lane, i_big, need_m);
+      load_L(nxt1, PL, M, A, i_mid1 + kLU * (d_nxt & kIdx) + 64 + lane, i_big, need_m);
     }
-    while (q_cur < n_q) {
+    uint32_t d_after = decode(claimed(claim()));
+    // the first unit's operands landed before the loop (an asm that reads
+    // them makes the compiler wait here), so on no path into the loop does a
+    // set's register still wait for a load
+    asm volatile("" ::"v"(nxt.p), "v"(nxt.a[0]), "v"(nxt.a[1]), "v"(nxt.a[2]), "v"(nxt.a[3]), "v"(nxt.a[4]),
+                 "v"(nxt.a[5]), "v"(nxt.a[6]), "v"(nxt.a[7]), "v"(nxt1.p), "v"(nxt1.a[0]), "v"(nxt1.a[1]),
+                 "v"(nxt1.a[2]), "v"(nxt1.a[3]), "v"(nxt1.a[4]), "v"(nxt1.a[5]), "v"(nxt1.a[6]), "v"(nxt1.a[7]));
+    for (;;) {
+      cur = nxt;
+      cur1 = nxt1;
+      undef_ops(nxt);  // dead until the next unit's loads: cur and nxt are never one register
+      undef_ops(nxt1);
+      const uint32_t d_cur = d_nxt;
+      d_nxt = d_after;
+      if (d_cur == ~0u) break;
       // issued and read in the same iteration: the asm output is written when
       // the LDS returns it, so the value must not be live across a loop phi
       // (a register copy there reads it early; a claim carried from one
       // iteration into the next gave wrong counts)
       const uint32_t c2 = claim();  // unit after next, read at the end of this one
-      if (q_nxt < n_q && unit_of(q_nxt) != ~0u && is_l(unit_of(q_nxt))) {
-        load_L(nxt, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_nxt)) + lane, i_big, need_m);
-        load_L(nxt1, P, M, A, i_mid1 + kLU * idx_of(unit_of(q_nxt)) + 64 + lane, i_big, need_m);
+      if ((d_nxt >> 30) == 1) {
+        load_L(nxt, PL, M, A, i_mid1 + kLU * (d_nxt & kIdx) + lane, i_big, need_m);
+        load_L(nxt1, PL, M, A, i_mid1 + kLU * (d_nxt & kIdx) + 64 + lane, i_big, need_m);
       }
-      const uint32_t u_cur = unit_of(q_cur);
-      if (BK && u_cur == ~0u) {  // a bucket unit, kBkBatchU loads in flight per lane
-        const uint32_t bu = bk_of(q_cur);
+      if (BK && (d_cur >> 30) == 2) {  // a bucket unit, kBkBatchU loads in flight per lane
+        const uint32_t bu = d_cur & kIdx;
         if (bu < n0u) {  // band 0: columns kBk0Lists bu .. +kBk0Lists, 4 at a time, each read by the whole wave
           const uint64_t li0 = s * (uint64_t)kBkGrid0 + bu * kBk0Lists;
           const uint32_t nl = lane < kBk0Lists ? wa.bk_n0[li0 + lane] : 0u;
@@ -1329,14 +1462,11 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
             if ((uint32_t)(v >> 32) == (uint32_t)s) mark_entry(img0, (uint32_t)v, one);
           }
         }
-        cur = nxt;
-        cur1 = nxt1;
-        q_cur = q_nxt;
-        q_nxt = claimed(c2);
+        d_after = decode(claimed(c2));
         continue;
       }
-      const uint32_t k = idx_of(u_cur);
-      if (!is_l(u_cur)) {
+      const uint32_t k = d_cur & kIdx;
+      if ((d_cur >> 30) == 0) {
         if (k < nA) {
           const uint32_t pi = __builtin_amdgcn_readfirstlane(s_mid_p[k]);
           const uint32_t p = pi & 0xFFFFu;
@@ -1355,15 +1485,13 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
             unit_B2(img0, s_mid_p, s_mid_m, mr, j0, min(8u, n_mid - j0), Vs, Vend, rg.rho_pack, lane, one);
         }
       } else {
-        const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p);
-        if ((uint64_t)p0 * p0 < Vend) unit_L<BK>(cur, Vs, Vend, Kb, ps, pl_rot, rg.rho_pack);
-        const uint32_t p1 = __builtin_amdgcn_readfirstlane(cur1.p);
-        if ((uint64_t)p1 * p1 < Vend) unit_L<BK>(cur1, Vs, Vend, Kb, ps, pl_rot, rg.rho_pack);
+        // a set marks if its first prime's square is below the segment's end
+        const uint32_t p0 = __builtin_amdgcn_readfirstlane(cur.p) & kLPrimeMask;
+        if (p0 <= sqrt_ve) unit_L<BK>(cur, Vs, Vend, Kb, ps, pl_rot, rho_pack_p, sqrt_vs);
+        const uint32_t p1 = __builtin_amdgcn_readfirstlane(cur1.p) & kLPrimeMask;
+        if (p1 <= sqrt_ve) unit_L<BK>(cur1, Vs, Vend, Kb, ps, pl_rot, rho_pack_p, sqrt_vs);
       }
-      cur = nxt;
-      cur1 = nxt1;
-      q_cur = q_nxt;
-      q_nxt = claimed(c2);
+      d_after = decode(claimed(c2));
     }
   };
 
@@ -1417,9 +1545,21 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
   const uint32_t* P = reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(table) + 16);
   uint64_t* M = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(table) + table_m_offset(h->cap));
   uint32_t* A = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + table_a_offset(h->cap));
+  uint32_t* PL = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + table_l_offset(h->cap));
+  static_assert(kWheelLogKP == 17, "pl[0] is the full geometry's, pl[1] the half geometry's");
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t p = P[i];
     if (p > kWheelMaxPrime) continue;  // bucketed primes: the walks divide in double precision
+    // the plans of the prime's set of 64 in the L list (unit_L), per geometry
+    uint32_t plan0 = 0, plan1 = 0;
+    if (i >= kL0) {
+      const uint32_t s0 = i - (i - kL0) % 64;
+      const uint32_t pmin = P[s0], pmax = P[min(s0 + 63, n - 1)];
+      plan0 = l_plan(pmin, pmax, 1u << 17);
+      plan1 = l_plan(pmin, pmax, 1u << 16);
+    }
+    PL[i] = p | plan0 << 20;
+    PL[h->cap + i] = p | plan1 << 20;
     const uint64_t m = barrett_factor(p);
     M[i] = m;
     if (p < 7) {
@@ -1438,8 +1578,10 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
 }
 
 // ---------------------------------------------------------------------------
-// Bucketed pass for the primes above kWheelMaxPrime (high-offset windows):
-// such a prime hits a 2 M-integer segment less than once, so instead of
+// Bucketed pass of the ranges whose sqrt(max value) exceeds kWheelMaxPrime
+// (high-offset windows) for their primes above 2^kBucketLoLog (or the
+// bucket_lo_log2 option): such a prime hits a 3.9 M-integer segment about
+// 2^20 / p times (at most twice), so instead of
 // visiting every (prime, segment) pair the kernels below walk each prime's
 // multiples p*m, gcd(m, 30) = 1, across the whole range once and file every
 // hit under its segment (bucket_entry). Band 0 (one level): each fill
@@ -1483,7 +1625,7 @@ struct BucketArgs {
   uint64_t plane_lut;  // plane of relative residue rho (odd) in bits [3(rho >> 1), +3)
   uint32_t nseg;       // segments in the pass (<= kBucketMaxSegs)
   uint64_t vmax;       // largest value of the pass (primes with p^2 > vmax have no hits)
-  uint64_t split;      // band 0: kWheelMaxPrime < p <= split, band 1: p > split
+  uint64_t split;      // band 0: 2^kBucketLoLog < p <= split, band 1: p > split
 };
 
 // Band-0 output of a pass (bucket_fill_wg).
@@ -2068,7 +2210,7 @@ namespace {
     *plane_lut |= (uint64_t)n << (3 * (rho >> 1));
     ++n;
   }
-  // primes 3..61 inside the range: the wheel drops 3 and 5, the patterns mark 7..61 themselves
+  // primes 3..79 inside the range: the wheel drops 3 and 5, the patterns mark 7..79 themselves
   constexpr uint32_t small[] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59, 61, 67, 71, 73, 79};
   static_assert(small[sizeof(small) / sizeof(small[0]) - 1] == kQMax && (kQMax - 3) / 2 < 64, "fix covers 3..kQMax");
   for (uint32_t v : small)
@@ -2086,7 +2228,7 @@ namespace {
 
 // A launch over the ranges rs[0..n) (1 <= n <= kMaxRanges, each < 2^31
 // segments in all), their segments in order; thresholds: odd primes up to
-// 61, TA, TB1, TB and wheel_max (<= kWheelMaxPrime: the primes above it are
+// kQMax, TA, TB1, TB and wheel_max (<= kWheelMaxPrime: the primes above it are
 // bucketed or absent).
 [[maybe_unused]] WheelArgs make_wheel_args(const RangeSpec* rs, uint32_t n, uint64_t* plane_lut,
                                            uint64_t wheel_max = kWheelMaxPrime) {
@@ -2148,7 +2290,9 @@ uint64_t bucket_cap(uint64_t span, double a, double b) {
 // round's first prime p(r), so its mean is at most lambda = (8 W / 30) sum_r
 // 256 / p(r) (p(r) from the table index i_lo + r S: p_n >= n (ln n + ln ln n
 // - 1), Dusart), and its variance at most lambda plus ~4 per prime below the
-// segment span W (~1 hit per prime there, +-2). k0 = lambda + 10 sigma + 64:
+// segment span W: such a prime (2^19 < p < W, all in round 0) hits each of
+// the 8 planes floor or ceil of KP / p times, a deviation of variance <= 1/4
+// per plane, 2 per prime (4 taken). k0 = lambda + 10 sigma + 64:
 // a region past it is a >10-sigma event, and even then its hits are spilled,
 // not lost.
 uint32_t bucket_k0(uint32_t i_lo, double a, double b) {
