@@ -241,7 +241,7 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x) {
 
 constexpr uint32_t kBlockMask = ~31u;  // period index -> its block's byte address
 #ifndef DSE_SHORT_TAIL
-#define DSE_SHORT_TAIL 8
+#define DSE_SHORT_TAIL 16
 #endif
 // MODE-0 L sets whose tail after the n_min run is at most this many steps mark
 // it unconditionally (past the segment: dropped) instead of in mark_tail's loop
@@ -910,7 +910,11 @@ __device__ __forceinline__ void unit_L(const LargeOps& o, uint64_t Vs, uint64_t 
   uint32_t kbm;
   if (Kb < (1ull << 32)) {
     const uint32_t q = (uint32_t)((float)(uint32_t)Kb * invp);
-    uint32_t x = (uint32_t)Kb - __umul24(q, p);  // in (-p, 2p) as a signed value; p < 2^24
+    // q p by v_mul_u32_u24 as asm: written as __umul24 the compiler merged it
+    // with the other path's product into one quarter-rate v_mul_lo_u32
+    uint32_t qp;
+    asm("v_mul_u32_u24 %0, %1, %2" : "=v"(qp) : "v"(q), "v"(p));
+    uint32_t x = (uint32_t)Kb - qp;  // in (-p, 2p) as a signed value; p < 2^24
     x = min(x, x + p);
     kbm = min(x, x - p);
   } else if (!BARRETT || Kb < (1ull << 38)) {
