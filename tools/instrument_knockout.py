@@ -42,8 +42,8 @@ def main(root):
             "if (!(DSE_KNOCK & 2) && (uint64_t)pf * pf < Vend)\n            unit_B1(")
     s = sub(s, "if ((uint64_t)pf * pf < Vend)\n            unit_B2(",
             "if (!(DSE_KNOCK & 4) && (uint64_t)pf * pf < Vend)\n            unit_B2(")
-    s = sub(s, "if ((uint64_t)p0 * p0 < Vend) unit_L(", "if (!(DSE_KNOCK & 8) && (uint64_t)p0 * p0 < Vend) unit_L(")
-    s = sub(s, "if ((uint64_t)p1 * p1 < Vend) unit_L(", "if (!(DSE_KNOCK & 8) && (uint64_t)p1 * p1 < Vend) unit_L(")
+    s = sub(s, "if (p0 <= sqrt_ve) unit_L<BK>(", "if (!(DSE_KNOCK & 8) && p0 <= sqrt_ve) unit_L<BK>(")
+    s = sub(s, "if (p1 <= sqrt_ve) unit_L<BK>(", "if (!(DSE_KNOCK & 8) && p1 <= sqrt_ve) unit_L<BK>(")
     s = sub(s, "    expand_segment(lds.img, s);\n", "    if (!(DSE_KNOCK & 16)) expand_segment(lds.img, s);\n")
     s = sub(s, "    if (t + 1 < T) init_segment(lds.img, s + grid);\n",
             "    if (!(DSE_KNOCK & 32) && t + 1 < T) init_segment(lds.img, s + grid);\n")
