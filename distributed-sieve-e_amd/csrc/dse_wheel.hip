@@ -1864,7 +1864,18 @@ __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const 
   for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) cur[j] = 0;
   __syncthreads();
   auto emit = [&](uint32_t sg, uint32_t e) {
+#if defined(DSE_BK_FILL_KO) && DSE_BK_FILL_KO == 3  // profiling knockout: the walk alone
+    asm volatile("" ::"v"(e), "v"(sg));
+    return;
+#endif
     const uint32_t pos = atomicAdd(&cur[sg], 1u);
+#if defined(DSE_BK_FILL_KO) && DSE_BK_FILL_KO == 1  // profiling knockout: no global store
+    asm volatile("" ::"v"(e), "v"(pos));
+    return;
+#elif defined(DSE_BK_FILL_KO) && DSE_BK_FILL_KO == 2  // profiling knockout: one coalesced line per store
+    bz.reg0[(uint64_t)b * kBucketThreads + threadIdx.x] = e + pos;
+    return;
+#endif
     if (pos < bz.k0) {
       bz.reg0[((uint64_t)sg * kBucketGrid + b) * bz.k0 + pos] = e;
     } else {
@@ -2062,6 +2073,11 @@ __global__ __launch_bounds__(kBucketThreads) void bucket_fill_stage_kernel(
       for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) bz.n0[(uint64_t)j * kBucketGrid + x] = 0;
     return;
   }
+#if defined(DSE_BK_FILL_KO) && DSE_BK_FILL_KO == 4  // profiling knockout: band-0 fill only
+  if (x >= nfill) return;
+#elif defined(DSE_BK_FILL_KO) && DSE_BK_FILL_KO == 5  // profiling knockout: band-1 staging only
+  if (x < nfill) return;
+#endif
   if (x < nfill)
     bucket_fill_wg(sm, x, table, ba, range, bz);
   else
@@ -2074,6 +2090,9 @@ __global__ __launch_bounds__(kSortThreads) void bucket_sort_kernel(BucketArgs ba
                                                                    uint32_t* __restrict__ entries,
                                                                    const uint32_t* __restrict__ flag) {
   if (flag[1]) return;  // capacity overflow (bucket_startscan_kernel)
+#if defined(DSE_BK_FILL_KO) && DSE_BK_FILL_KO == 4  // profiling knockout: nothing staged to sort
+  return;
+#endif
   constexpr uint32_t kPer = kSortTile / kSortThreads;
   constexpr uint32_t kPerLane = kSupSegs / 64;  // scan: segment counts per lane of wave 0
   __shared__ uint32_t sorted[kSortTile];
