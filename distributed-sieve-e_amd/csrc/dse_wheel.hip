@@ -209,7 +209,7 @@ struct WheelArgs {
   const uint32_t* bk_entries;  // band 1: segment s owns [bk_start[s], bk_start[s+1])
   const uint32_t* bk_start;
   const uint32_t* bk_reg0;     // band 0: segment s, column b: bk_n0[s * kBucketGrid + b] entries
-  const uint32_t* bk_n0;       //   from bk_reg0 + (s * kBucketGrid + b) * bk_k0
+  const uint32_t* bk_n0;       //   from bk_reg0 + (b * nseg + s) * bk_k0
   const unsigned long long* bk_spill;  // band-0 hits past their region: segment << 32 | entry,
   const uint32_t* bk_nspill;           //   *bk_nspill of them (normally none)
   uint64_t bk_spill_cap;               //   (at most this many stored)
@@ -1431,7 +1431,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
 #pragma unroll
             for (uint32_t l = 0; l < 4; ++l) {
               n[l] = min((uint32_t)__builtin_amdgcn_readlane((int)nl, (int)(g + l)), wa.bk_k0);
-              r[l] = wa.bk_reg0 + (li0 + g + l) * wa.bk_k0;
+              r[l] = wa.bk_reg0 + ((uint64_t)(bu * kBk0Lists + g + l) * wa.nseg + s) * wa.bk_k0;
               nmax = max(nmax, n[l]);
             }
             for (uint32_t o = lane; o < nmax + lane; o += 256) {  // contiguous 256-entry pieces of 4 lists
@@ -1634,7 +1634,7 @@ struct BucketArgs {
 
 // Band-0 output of a pass (bucket_fill_wg).
 struct BandZero {
-  uint32_t* reg0;                  // [nseg][kBucketGrid][k0] regions
+  uint32_t* reg0;                  // [kBucketGrid][nseg][k0] regions
   uint32_t* n0;                    // [nseg][kBucketGrid] region fills
   unsigned long long* spill;       // segment << 32 | entry
   uint32_t* nspill;                // spill list length
@@ -1845,16 +1845,58 @@ __global__ __launch_bounds__(1024) void bucket_startscan_kernel(const uint32_t* 
 constexpr uint32_t kFillRG = DSE_BK_FILL_RG;  // stride rounds of primes walked together
 
 // Band 0, one-level fill: every hit is one dword store at its slot. Workgroup
-// b owns region (s, b) of every segment s: k0 slots at reg0 + (s kBucketGrid +
-// b) k0, slot = an LDS cursor per segment. No count pass: k0 bounds the
-// region's expected fill by many standard deviations (bucket_k0), and a hit
-// past it goes to the spill list (a global atomic; the list's capacity is a
-// rigorous bound on the band's hits), so nothing is dropped whatever k0 is.
-// The lanes of a wave walk consecutive primes, so for small p a step's hits
-// share a segment and take consecutive slots (one coalesced store); the
-// larger the primes, the more a step's stores scatter (2.7 ps per hit below
-// 2^24, 12 ps above 2^28 at the 1e18 window), hence band 1. At the end the
-// region fills go to n0[s kBucketGrid + b] (capped at k0).
+// b owns region (s, b) of every segment s: k0 slots at reg0 + (b nseg + s) k0
+// (a workgroup's regions are contiguous, so a slot is a 32-bit offset from
+// one scalar base), slot = an LDS cursor per segment. No count pass: k0
+// bounds the region's expected fill by many standard deviations (bucket_k0),
+// and a hit past it goes to the spill list (a global atomic; the list's
+// capacity is a rigorous bound on the band's hits), so nothing is dropped
+// whatever k0 is. At the end the region fills go to n0[s kBucketGrid + b]
+// (capped at k0).
+//
+// The walk is issue-bound (profiles/r06/window_fill_knockouts.txt: without
+// its atomics and stores it still takes 2/3 of the fill's time), so a hit
+// costs as few VALU as the walk allows: a prime's state is its period index
+// k = o / 30 from V0 (32 bits: a pass spans < 2^30 periods) and its wheel
+// step w, kept as w4 = 4 w; everything that depends on the step comes from
+// 4-bit fields at bit 4 w (v_bfe reads only the low 5 bits of the offset, so
+// w4 just counts up): the gap, the carry of the residue, and the plane. With
+// p = 30 pq + pm and residue rho_w of step w, the next hit is
+// k + pq gap_w + (rho_w + pm gap_w) / 30; bucket_fill_start builds the carry
+// and plane fields once per prime (eight residues from the first hit's).
+constexpr uint64_t kFillMaxSplit = 30ull << 24;  // band-0 primes p < 30 * 2^24: p / 30 < 2^24 (v_mul_u32_u24)
+static_assert((1ull << kBucketSplitLog) <= kFillMaxSplit, "production split");
+constexpr uint32_t kGap30x4 = 6u | (4u << 4) | (2u << 8) | (4u << 12) | (2u << 16) | (4u << 20) | (6u << 24) | (2u << 28);
+
+struct FillWalk {
+  uint32_t k;       // period index of the next hit from V0 (~0u: none left in the pass)
+  uint32_t w4;      // 4 * wheel step (mod 32 as used)
+  uint32_t pq;      // p / 30
+  uint32_t carry;   // 4-bit fields: (rho_w + pm gap_w) / 30
+  uint32_t plane;   // 4-bit fields: plane of rho_w
+};
+
+__device__ __forceinline__ FillWalk bucket_fill_start(uint32_t p, const BucketArgs& ba) {
+  uint32_t w3;
+  const uint64_t o = bucket_first(p, ba, w3);
+  FillWalk f{~0u, 0u, p / 30u, 0u, 0u};
+  if (o >= ba.span) return f;
+  const uint32_t kq = (uint32_t)(o / 30u);  // o < span + 6 p < 2^36: kq < 2^31
+  uint32_t rho = (uint32_t)(o - 30ull * kq);
+  const uint32_t w0 = w3 / 3u, pm = p - 30u * f.pq;
+  f.k = kq;
+  f.w4 = 4u * w0;
+  for (uint32_t j = 0; j < 8; ++j) {
+    const uint32_t w = (w0 + j) & 7u, gap = (kGap30x4 >> (4u * w)) & 15u;
+    const uint32_t t = rho + pm * gap;  // < 30 + 29 * 6
+    const uint32_t c = t / 30u;
+    f.carry |= c << (4u * w);
+    f.plane |= ((uint32_t)(ba.plane_lut >> (3u * (rho >> 1))) & 7u) << (4u * w);
+    rho = t - 30u * c;
+  }
+  return f;
+}
+
 // (band-0 workgroup b; cur: nseg words of LDS)
 __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const void* __restrict__ table,
                                                const BucketArgs& ba, const uint32_t* __restrict__ range,
@@ -1863,6 +1905,8 @@ __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const 
   const uint32_t i_lo = range[0], i_hi = range[2];
   for (uint32_t j = threadIdx.x; j < ba.nseg; j += kBucketThreads) cur[j] = 0;
   __syncthreads();
+  char* const reg_b = reinterpret_cast<char*>(bz.reg0 + (uint64_t)b * ba.nseg * bz.k0);  // this workgroup's regions
+  const uint32_t k0 = bz.k0;
   auto emit = [&](uint32_t sg, uint32_t e) {
 #if defined(DSE_BK_FILL_KO) && DSE_BK_FILL_KO == 3  // profiling knockout: the walk alone
     asm volatile("" ::"v"(e), "v"(sg));
@@ -1876,8 +1920,8 @@ __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const 
     bz.reg0[(uint64_t)b * kBucketThreads + threadIdx.x] = e + pos;
     return;
 #endif
-    if (pos < bz.k0) {
-      bz.reg0[((uint64_t)sg * kBucketGrid + b) * bz.k0 + pos] = e;
+    if (pos < k0) {
+      *reinterpret_cast<uint32_t*>(reg_b + 4u * (__umul24(sg, k0) + pos)) = e;  // < 2^32: per-workgroup regions
     } else {
       const uint32_t j = atomicAdd(bz.nspill, 1u);
       if (j < bz.spill_cap) {
@@ -1897,36 +1941,38 @@ __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const 
   // plain order the threads holding a band's smallest primes walk up to
   // ~1.7x the mean).
   constexpr uint32_t stride = kBucketGrid * kBucketThreads;
+  constexpr uint32_t kKPMask = (1u << kWheelLogKP) - 1;
   const uint32_t j = b * kBucketThreads + threadIdx.x;
   const uint32_t jr = stride - 1 - j;
-  const uint64_t chunk = (uint64_t)DSE_BK_CHUNK * kWheelSpan;
+  const uint32_t kspan = ba.nseg << kWheelLogKP;  // periods of the pass (< 2^30)
   for (uint64_t r0 = 0; i_lo + r0 * stride < i_hi; r0 += kFillRG) {
-    uint64_t o[kFillRG];
-    uint32_t pr[kFillRG], w3[kFillRG];
+    FillWalk f[kFillRG];
 #pragma unroll
     for (uint32_t r = 0; r < kFillRG; ++r) {
       const uint64_t i = i_lo + (r0 + r) * stride + (((r0 + r) & 1) ? jr : j);
-      o[r] = ba.span;
-      pr[r] = 0;
-      w3[r] = 0;
-      if (i < i_hi) {
-        pr[r] = P[i];
-        o[r] = bucket_first(pr[r], ba, w3[r]);
-      }
+      f[r] = FillWalk{~0u, 0u, 0u, 0u, 0u};
+      if (i < i_hi) f[r] = bucket_fill_start(P[i], ba);
     }
-    for (uint64_t end = chunk;; end += chunk) {
-      const uint64_t lim = min(end, ba.span);
+#ifndef DSE_BK_CHUNK_GROW
+#define DSE_BK_CHUNK_GROW 0
+#endif
+    const uint32_t cseg = DSE_BK_CHUNK << min(3u, (uint32_t)(r0 / kFillRG) * DSE_BK_CHUNK_GROW);
+    for (uint32_t end = cseg;; end += cseg) {
+      const uint32_t klim = min(end << kWheelLogKP, kspan);
       bool left = false;
 #pragma unroll
       for (uint32_t r = 0; r < kFillRG; ++r) {
-        while (o[r] < lim) {
-          uint32_t sg;
-          const uint32_t e = bucket_entry(o[r], ba, sg);
-          emit(sg, e);
-          o[r] += (uint64_t)pr[r] * ((kGap30 >> w3[r]) & 7u);
-          w3[r] = w3[r] == 21 ? 0u : w3[r] + 3;
+        while (f[r].k < klim) {
+          const uint32_t k = f[r].k, w4 = f[r].w4;
+          const uint32_t pl = __builtin_amdgcn_ubfe(f[r].plane, w4, 4);
+          const uint32_t gap = __builtin_amdgcn_ubfe(kGap30x4, w4, 4);
+          const uint32_t c = __builtin_amdgcn_ubfe(f[r].carry, w4, 4);
+          // entry (bucket_entry): LDS word (block << 3 | plane) << 5 | bit
+          emit(k >> kWheelLogKP, ((k & kKPMask & ~31u) << 3) | (pl << 5) | (k & 31u));
+          f[r].k = k + __umul24(f[r].pq, gap) + c;  // pq < 2^24
+          f[r].w4 = w4 + 4u;
         }
-        left |= o[r] < ba.span;
+        left |= f[r].k < kspan;
       }
       if (!left) break;
     }
@@ -2477,7 +2523,9 @@ hipError_t launch_bucketed(const void* table, uint64_t g_start, uint64_t nbits, 
   const uint64_t total_seg = (nbits + kWheelOutBits - 1) / kWheelOutBits;
   uint64_t max_segs = kBucketMaxSegs;
   if (opts && opts->bucket_pass_segs >= 1 && opts->bucket_pass_segs < max_segs) max_segs = opts->bucket_pass_segs;
-  const uint64_t split = 1ull << (opts && opts->bucket_split_log2 ? opts->bucket_split_log2 : kBucketSplitLog);
+  // band 0 stops below 30 * 2^24 whatever the option (its walk's 24-bit step product, bucket_fill_wg)
+  const uint64_t split =
+      std::min<uint64_t>(1ull << (opts && opts->bucket_split_log2 ? opts->bucket_split_log2 : kBucketSplitLog), kFillMaxSplit);
   // primes above lo_p are bucketed: below kWheelMaxPrime for a range that is
   // bucketed anyway (a prime that hits a segment about once is cheaper as a
   // bucket entry than as 8 plane slots of an L unit; window: 2^19 -2%)
@@ -2498,6 +2546,7 @@ hipError_t launch_bucketed(const void* table, uint64_t g_start, uint64_t nbits, 
     const uint64_t vmax_p = 3 + 2 * (g0 + nb - 1);
     piece = {g0, nb, out ? out + s0 * (kWheelOutBits / 32) : nullptr, count};
     wa = make_wheel_args(&piece, 1, &plane_lut, lo_p);
+    if (wa.nseg != ns) return hipErrorInvalidValue;  // the band-0 region layout's nseg (wheel side: wa.nseg)
     BucketArgs ba{};
     ba.V0 = wa.r[0].V0;
     ba.span = ns * kWheelSpan;
