@@ -1837,7 +1837,10 @@ __global__ __launch_bounds__(1024) void bucket_startscan_kernel(const uint32_t* 
 }
 
 #ifndef DSE_BK_CHUNK
-#define DSE_BK_CHUNK 32  // band-0 fill walks chunks of this many segments
+#define DSE_BK_CHUNK 16  // band-0 fill walks chunks of this many segments (first group of kFillRG rounds) ...
+#endif
+#ifndef DSE_BK_CHUNK_GROW
+#define DSE_BK_CHUNK_GROW 1  // ... doubled for each later group, up to 8x (profiles/r06/window_fill_chunks.txt)
 #endif
 #ifndef DSE_BK_FILL_RG
 #define DSE_BK_FILL_RG 16
@@ -1907,6 +1910,20 @@ __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const 
   __syncthreads();
   char* const reg_b = reinterpret_cast<char*>(bz.reg0 + (uint64_t)b * ba.nseg * bz.k0);  // this workgroup's regions
   const uint32_t k0 = bz.k0;
+  // slot pos of region (sg, b), or the spill list past its capacity
+  auto put = [&](uint32_t sg, uint32_t pos, uint32_t e) {
+    if (pos < k0) {
+      *reinterpret_cast<uint32_t*>(reg_b + 4u * (__umul24(sg, k0) + pos)) = e;  // < 2^32: per-workgroup regions
+    } else {
+      const uint32_t j = atomicAdd(bz.nspill, 1u);
+      if (j < bz.spill_cap) {
+        bz.spill[j] = (unsigned long long)sg << 32 | e;
+      } else {  // only with a test-shrunk capacity (bucket_cap_divisor): fail loudly
+        bz.flag[0] = 1u;
+        atomicOr(bz.count, 1ull << 63);
+      }
+    }
+  };
   auto emit = [&](uint32_t sg, uint32_t e) {
 #if defined(DSE_BK_FILL_KO) && DSE_BK_FILL_KO == 3  // profiling knockout: the walk alone
     asm volatile("" ::"v"(e), "v"(sg));
@@ -1920,17 +1937,7 @@ __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const 
     bz.reg0[(uint64_t)b * kBucketThreads + threadIdx.x] = e + pos;
     return;
 #endif
-    if (pos < k0) {
-      *reinterpret_cast<uint32_t*>(reg_b + 4u * (__umul24(sg, k0) + pos)) = e;  // < 2^32: per-workgroup regions
-    } else {
-      const uint32_t j = atomicAdd(bz.nspill, 1u);
-      if (j < bz.spill_cap) {
-        bz.spill[j] = (unsigned long long)sg << 32 | e;
-      } else {  // only with a test-shrunk capacity (bucket_cap_divisor): fail loudly
-        bz.flag[0] = 1u;
-        atomicOr(bz.count, 1ull << 63);
-      }
-    }
+    put(sg, pos, e);
   };
   // Segment-ordered walk: a thread walks its primes of kFillRG stride rounds
   // together, chunk by chunk of DSE_BK_CHUNK segments, so region (s, b) gets
@@ -1953,9 +1960,8 @@ __device__ __forceinline__ void bucket_fill_wg(uint32_t* cur, uint32_t b, const 
       f[r] = FillWalk{~0u, 0u, 0u, 0u, 0u};
       if (i < i_hi) f[r] = bucket_fill_start(P[i], ba);
     }
-#ifndef DSE_BK_CHUNK_GROW
-#define DSE_BK_CHUNK_GROW 0
-#endif
+    // later groups walk larger primes (fewer hits per chunk: lanes idle in
+    // the divergent walk) at larger chunks
     const uint32_t cseg = DSE_BK_CHUNK << min(3u, (uint32_t)(r0 / kFillRG) * DSE_BK_CHUNK_GROW);
     for (uint32_t end = cseg;; end += cseg) {
       const uint32_t klim = min(end << kWheelLogKP, kspan);
