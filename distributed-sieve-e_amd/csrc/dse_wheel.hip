@@ -240,6 +240,11 @@ __device__ __forceinline__ uint32_t opaque(uint32_t x) {
 }
 
 constexpr uint32_t kBlockMask = ~31u;  // period index -> its block's byte address
+#ifndef DSE_FAKE_CF_L
+#define DSE_FAKE_CF_L 0
+#endif
+// profiling knockout (DSE_FAKE_CF_L): the L marks' blocks forced to lane-distinct banks (wrong marks)
+constexpr uint32_t kBlockMaskL = DSE_FAKE_CF_L ? ~127u : kBlockMask;
 #ifndef DSE_SHORT_TAIL
 #define DSE_SHORT_TAIL 16
 #endif
@@ -819,7 +824,7 @@ __device__ __forceinline__ void start_marks4(const uint32_t* a, const uint32_t* 
         DSE_PLANE_START("%6", "%10") DSE_PLANE_MARK("%14")
         : "=&v"(t), "=&v"(u), "=&v"(b)
         : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(ne[0]), "v"(ne[1]), "v"(ne[2]), "v"(ne[3]), "v"(pb[0]),
-          "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(nKbm), "v"(p), "s"(kBlockMask), "v"(one)
+          "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(nKbm), "v"(p), "s"(kBlockMaskL), "v"(one)
         : "memory");
   else
     asm volatile(
@@ -829,7 +834,7 @@ __device__ __forceinline__ void start_marks4(const uint32_t* a, const uint32_t* 
         DSE_PLANE_START("%6", "%10") DSE_PLANE_MARK("%14") DSE_PLANE_NEXT DSE_PLANE_MARK("%14")
         : "=&v"(t), "=&v"(u), "=&v"(b)
         : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(ne[0]), "v"(ne[1]), "v"(ne[2]), "v"(ne[3]), "v"(pb[0]),
-          "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(nKbm), "v"(p), "s"(kBlockMask), "v"(one)
+          "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(nKbm), "v"(p), "s"(kBlockMaskL), "v"(one)
         : "memory");
 }
 
@@ -853,7 +858,7 @@ __device__ __forceinline__ void mark8(uint32_t (&k)[8], const uint32_t* pb, uint
                : "=&v"(a0), "=&v"(b0), "=&v"(a1), "=&v"(b1), "+v"(k[0]), "+v"(k[1]), "+v"(k[2]), "+v"(k[3]),
                  "+v"(k[4]), "+v"(k[5]), "+v"(k[6]), "+v"(k[7])
                : "v"(pb[0]), "v"(pb[1]), "v"(pb[2]), "v"(pb[3]), "v"(pb[4]), "v"(pb[5]), "v"(pb[6]), "v"(pb[7]),
-                 "v"(p), "s"(kBlockMask), "v"(one)
+                 "v"(p), "s"(kBlockMaskL), "v"(one)
                : "memory");
 }
 
@@ -1332,7 +1337,7 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     ps.one = one;
 #pragma unroll
     for (uint32_t q = 0; q < 8; ++q) {
-      ps.pb[q] = img0 + 4 * ((pl_rot >> (3 * q)) & 7u);
+      ps.pb[q] = img0 + 4 * ((pl_rot >> (3 * q)) & 7u) + (DSE_FAKE_CF_L ? ((lane_id >> 3) & 3u) << 5 : 0u);
       ps.ne[q] = 0u - ((e_rot >> q) & 1u);
     }
     const uint64_t Kb = rg.KB0 + s * (uint64_t)KP;
@@ -1553,7 +1558,7 @@ __global__ void wheel_offsets_kernel(void* __restrict__ table) {
   static_assert(kWheelLogKP == 17, "pl[0] is the full geometry's, pl[1] the half geometry's");
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const uint32_t p = P[i];
-    if (p > kWheelMaxPrime) continue;  // bucketed primes: the walks divide in double precision
+    if (p > kWheelMaxPrime) break;  // bucketed primes (P ascends: all later ones too): the walks divide in double precision
     // the plans of the prime's set of 64 in the L list (unit_L), per geometry
     uint32_t plan0 = 0, plan1 = 0;
     if (i >= kL0) {
@@ -2236,6 +2241,10 @@ __global__ __launch_bounds__(kSortThreads) void bucket_sort_kernel(BucketArgs ba
 
 #if DSE_WHEEL_MAIN_TU
 hipError_t launch_wheel_offsets(void* table, int num_cus, hipStream_t stream, uint64_t n_hint) {
+  // rows, factors and plans only for the primes <= kWheelMaxPrime (82,025 below 2^20): the kernel stops
+  // at the first bucketed prime, so a window's 50.8 M-prime table needs no larger grid (the grid-stride
+  // loop covers every index whatever the grid)
+  n_hint = std::min<uint64_t>(n_hint, 1u << 17);
   const uint64_t grid = std::max<uint64_t>(4 * (uint64_t)num_cus, std::min<uint64_t>(n_hint / 1024 + 1, 1u << 16));
   hipLaunchKernelGGL(wheel_offsets_kernel, dim3((uint32_t)grid), dim3(256), 0, stream, table);
   return hipGetLastError();
