@@ -117,6 +117,19 @@ def cpu_baseline(max_n: int, reps: int = 3) -> dict:
             "runs": runs}
 
 
+def lib_build():
+    """The library this run loaded: its path and the first 16 hex digits of its
+    SHA-256, the id that profiles/<round>/pmc_build.json records for the build
+    its traces and counters were taken from (so a line, e.g. the one printed
+    under a rocprofv3 trace, names its own build)."""
+    import hashlib
+    from mail_sieve_e import _dse
+    path = _dse.LIB_PATH
+    with open(path, "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()[:16]
+    return {"libdse": os.path.relpath(path, ROOT), "libdse_sha256_16": sha}
+
+
 def pmc_summary(N: int, P: int, window: bool):
     """Per-launch figures of the sieve kernel from the committed rocprofv3 PMC
     passes for this config (profiles/<round>/pmc_*_sieve_kernel.csv, N=1e11,
@@ -470,6 +483,7 @@ def run(a, world: int, rank: int, wd: Watchdog):
             "roofline": None,
             "cpu_baseline": None,
             "world": world_info,
+            "build": lib_build(),
         }
         if a.window:
             out["roofline"] = window_roofline
@@ -511,6 +525,7 @@ def run(a, world: int, rank: int, wd: Watchdog):
                 "pmc_committed": None if not pmc else {
                     "source": pmc["source"],
                     "build": pmc["build"],
+                    "same_build": bool(pmc["build"]) and pmc["build"].get("libdse_sha256_16") == out["build"]["libdse_sha256_16"],
                     "traffic": pmc["traffic"],
                     "hbm_frac": pmc["traffic"] / ks / 1e9 / work.HBM_PEAK_GBS,
                     "cycles_per_cu": pmc["cycles"],

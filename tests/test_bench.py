@@ -45,6 +45,8 @@ def _check_line(d: dict, n_gpus: int):
     # the headline is the median of per-step times, each from the call to the counts on the host
     assert d["ms_per_step"] > 0 and d["ms_per_step_bracketed"] > 0 and d["ms_per_step_pipelined"] > 0
     assert abs(d["value"] - d["config"]["N"] / (d["ms_per_step"] / 1e3)) < 1e-6 * d["value"]
+    # the line names the library it loaded (the id pmc_build.json records for a profiled build)
+    assert d["build"]["libdse"].endswith("libdse.so") and len(d["build"]["libdse_sha256_16"]) == 16
 
 
 @pytest.mark.gpu
@@ -142,3 +144,15 @@ def test_watchdog_names_rank_and_phase():
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT)
     assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
     assert "bench.py rank 1/8 in phase 'timed steps': no progress for 1 s" in r.stderr
+
+
+def test_lib_build_id_is_the_library_sha():
+    """bench.lib_build(): the loaded library's path and SHA-256 prefix (CPU only:
+    hashing the file, no GPU call)."""
+    import hashlib
+    sys.path.insert(0, ROOT)
+    import bench
+    b = bench.lib_build()
+    path = os.path.join(ROOT, b["libdse"])
+    assert os.path.exists(path)
+    assert b["libdse_sha256_16"] == hashlib.sha256(open(path, "rb").read()).hexdigest()[:16]
