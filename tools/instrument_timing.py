@@ -46,20 +46,20 @@ def main(root):
             "#define DSE_TSTAMP(i) do { const uint64_t t_now = __builtin_amdgcn_s_memtime();"
             " if ((i) >= 0) t_acc[i] += t_now - t_prev; t_prev = t_now; } while (0)\n")
     # unit attribution (LDS drained after each unit)
-    s = sub(s, "      const uint32_t k = idx_of(u_cur);\n      if (!is_l(u_cur)) {\n",
-            "      const uint32_t k = idx_of(u_cur);\n"
+    s = sub(s, "      const uint32_t k = d_cur & kIdx;\n      if ((d_cur >> 30) == 0) {\n",
+            "      const uint32_t k = d_cur & kIdx;\n"
             "      const uint64_t t_u0 = __builtin_amdgcn_s_memtime();\n"
-            "      const uint32_t u_type = !is_l(u_cur) ? (k < nA ? 5u : k < nA + nB1 ? 6u : 7u) : 8u;\n"
-            "      if (!is_l(u_cur)) {\n")
-    s = sub(s, "      cur = nxt;\n      cur1 = nxt1;\n      q_cur = q_nxt;\n      q_nxt = claimed(c2);\n    }\n  };",
-            "      lds_drain();\n      t_acc[u_type] += __builtin_amdgcn_s_memtime() - t_u0;\n"
-            "      cur = nxt;\n      cur1 = nxt1;\n      q_cur = q_nxt;\n      q_nxt = claimed(c2);\n    }\n  };")
-    s = sub(s, "      if (BK && u_cur == ~0u) {  // a bucket unit, kBkBatchU loads in flight per lane\n",
-            "      if (BK && u_cur == ~0u) {  // a bucket unit, kBkBatchU loads in flight per lane\n"
+            "      const uint32_t u_type = (d_cur >> 30) == 0 ? (k < nA ? 5u : k < nA + nB1 ? 6u : 7u) : 8u;\n"
+            "      if ((d_cur >> 30) == 0) {\n")
+    s = sub(s, "      }\n      d_after = decode(claimed(c2));\n    }\n  };",
+            "      }\n      lds_drain();\n      t_acc[u_type] += __builtin_amdgcn_s_memtime() - t_u0;\n"
+            "      d_after = decode(claimed(c2));\n    }\n  };")
+    s = sub(s, "      if (BK && (d_cur >> 30) == 2) {  // a bucket unit, kBkBatchU loads in flight per lane\n",
+            "      if (BK && (d_cur >> 30) == 2) {  // a bucket unit, kBkBatchU loads in flight per lane\n"
             "        const uint64_t t_b0 = __builtin_amdgcn_s_memtime();\n")
-    s = sub(s, "        cur = nxt;\n        cur1 = nxt1;\n        q_cur = q_nxt;\n        q_nxt = claimed(c2);\n        continue;",
+    s = sub(s, "        d_after = decode(claimed(c2));\n        continue;",
             "        lds_drain();\n        t_acc[9] += __builtin_amdgcn_s_memtime() - t_b0;\n"
-            "        cur = nxt;\n        cur1 = nxt1;\n        q_cur = q_nxt;\n        q_nxt = claimed(c2);\n        continue;")
+            "        d_after = decode(claimed(c2));\n        continue;")
     # phases of the segment loop
     s = sub(s, "  if (T > 0) init_segment(lds.img, blockIdx.x);\n  __syncthreads();\n",
             "  if (T > 0) init_segment(lds.img, blockIdx.x);\n  __syncthreads();\n  DSE_TSTAMP(-1);\n")
