@@ -245,15 +245,6 @@ constexpr uint32_t kBlockMask = ~31u;  // period index -> its block's byte addre
 #endif
 // profiling knockout (DSE_FAKE_CF_L): the L marks' blocks forced to lane-distinct banks (wrong marks)
 constexpr uint32_t kBlockMaskL = DSE_FAKE_CF_L ? ~127u : kBlockMask;
-#ifndef DSE_GCLAIM
-#define DSE_GCLAIM 0
-#endif
-#if DSE_GCLAIM
-__device__ uint32_t g_claim_ctr[4096];  // experiment: per-workgroup unit-queue counters
-#endif
-#ifndef DSE_CLAIM_WAIT
-#define DSE_CLAIM_WAIT 0
-#endif
 #ifndef DSE_SHORT_TAIL
 #define DSE_SHORT_TAIL 16
 #endif
@@ -1068,10 +1059,6 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     s_thr[2] = min(s_thr[2], s_thr[3]);
     s_thr[4] = max(s_thr[3], min(wa.nthr[4], np));
     lds.ctr = 0;
-#if DSE_GCLAIM
-    __hip_atomic_store(&g_claim_ctr[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __threadfence();
-#endif
     lds.x_seg = ~0u;
   }
   if (tid < kMaxRanges) lds.rcnt[tid] = 0;
@@ -1373,18 +1360,6 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     // on the spot (draining the previous unit's marks with it), which
     // defeats the two-ahead issue. Read through claimed().
     const uint32_t ctr_addr = lds_addr(&lds.ctr);
-#if DSE_GCLAIM
-    // experiment: the claim counter in global memory, so reading a claim
-    // waits on vmcnt (with the next unit's operand loads) instead of
-    // draining the wave's LDS marks
-    (void)ctr_addr;
-    auto claim = [&]() -> uint32_t {
-      uint32_t j = 0;
-      if (lane == 0) j = __hip_atomic_fetch_add(&g_claim_ctr[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return j;
-    };
-    auto claimed = [&](uint32_t j) -> uint32_t { return __builtin_amdgcn_readlane(j, 0); };
-#else
     auto claim = [&]() -> uint32_t {
       uint32_t j = 0;
       if (lane == 0) asm volatile("ds_add_rtn_u32 %0, %1, %2" : "=v"(j) : "v"(ctr_addr), "v"(1u) : "memory");
@@ -1394,21 +1369,6 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(j)::"memory");
       return __builtin_amdgcn_readlane(j, 0);
     };
-#endif
-#if DSE_CLAIM_WAIT
-    // experiment: LDS instructions complete in order, so a claim issued
-    // before `after` (wave-uniform) further LDS instructions has returned
-    // once at most `after` are outstanding: wait for that, not for all
-    auto claimed_after = [&](uint32_t j, uint32_t after) -> uint32_t {
-      if (after >= 15)
-        asm volatile("s_waitcnt lgkmcnt(15)" : "+v"(j)::"memory");
-      else if (after >= 8)
-        asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(j)::"memory");
-      else
-        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(j)::"memory");
-      return __builtin_amdgcn_readlane(j, 0);
-    };
-#endif
     auto is_l = [&](uint32_t u) -> bool { return u < 2 * n_int ? (u & 1) != 0 : n2 > n1; };
     auto idx_of = [&](uint32_t u) -> uint32_t { return u < 2 * n_int ? u >> 1 : u - n_int; };
     // queue position -> marking unit (or ~0u: bucket unit bk_of(q)); the n3
@@ -1515,33 +1475,23 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         continue;
       }
       const uint32_t k = d_cur & kIdx;
-      uint32_t after = 0;  // LDS instructions issued after the claim c2, at least (DSE_CLAIM_WAIT)
       if ((d_cur >> 30) == 0) {
         if (k < nA) {
           const uint32_t pi = __builtin_amdgcn_readfirstlane(s_mid_p[k]);
           const uint32_t p = pi & 0xFFFFu;
           const uint64_t m = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s_mid_m[k] >> 32)) << 32) |
                              (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s_mid_m[k]);
-          if ((uint64_t)p * p < Vend) {
-            unit_A(img0, pi, m, mr, k, Vs, rg.rho_pack, lane, one);
-            if ((uint64_t)p * p <= Vs) after = 15;  // past p^2: 32 classes of >= 5 marks per lane
-          }
+          if ((uint64_t)p * p < Vend) unit_A(img0, pi, m, mr, k, Vs, rg.rho_pack, lane, one);
         } else if (k < nA + nB1) {
           const uint32_t j0 = nA + (k - nA) * 2;
           const uint32_t pf = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
-          if ((uint64_t)pf * pf < Vend) {
+          if ((uint64_t)pf * pf < Vend)
             unit_B1(img0, s_mid_p, s_mid_m, mr, j0, min(2u, n_b1 - j0), Vs, rg.rho_pack, lane, one);
-            const uint32_t pl = __builtin_amdgcn_readfirstlane(s_mid_p[j0 + min(2u, n_b1 - j0) - 1]) & 0xFFFFu;
-            if ((uint64_t)pl * pl <= Vs) after = 15;  // every prime past p^2: >= 64 hits per lane
-          }
         } else {
           const uint32_t j0 = n_b1 + (k - nA - nB1) * 8;
           const uint32_t pf = __builtin_amdgcn_readfirstlane(s_mid_p[j0]) & 0xFFFFu;
-          if ((uint64_t)pf * pf < Vend) {
+          if ((uint64_t)pf * pf < Vend)
             unit_B2(img0, s_mid_p, s_mid_m, mr, j0, min(8u, n_mid - j0), Vs, Vend, rg.rho_pack, lane, one);
-            const uint32_t pl = __builtin_amdgcn_readfirstlane(s_mid_p[j0 + min(8u, n_mid - j0) - 1]) & 0xFFFFu;
-            if ((uint64_t)pl * pl <= Vs) after = 15;  // every prime past p^2: >= 85 unconditional marks
-          }
         }
       } else {
         // a set marks if its first prime's square is below the segment's end
@@ -1549,17 +1499,8 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
         if (p0 <= sqrt_ve) unit_L<BK>(cur, Vs, Vend, Kb, ps, pl_rot, rho_pack_p, sqrt_vs);
         const uint32_t p1 = __builtin_amdgcn_readfirstlane(cur1.p) & kLPrimeMask;
         if (p1 <= sqrt_ve) unit_L<BK>(cur1, Vs, Vend, Kb, ps, pl_rot, rho_pack_p, sqrt_vs);
-        // a live set on the branch-free path (every prime past p^2: pmax <= isqrt(Vs)) issues >= 8 marks
-        const uint32_t q0 = __builtin_amdgcn_readlane(cur.p, 63) & kLPrimeMask;
-        const uint32_t q1 = __builtin_amdgcn_readlane(cur1.p, 63) & kLPrimeMask;
-        after = 8 * ((p0 <= sqrt_ve && q0 <= sqrt_vs) + (p1 <= sqrt_ve && q1 <= sqrt_vs));
       }
-#if DSE_CLAIM_WAIT
-      d_after = decode(claimed_after(c2, after));
-#else
-      (void)after;
       d_after = decode(claimed(c2));
-#endif
     }
   };
 
@@ -1577,10 +1518,6 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
     if (t + 1 < T) init_segment(lds.img, s + grid);
     if (tid == 0) {
       lds.ctr = 0;  // all claims of this segment returned before the barrier above
-#if DSE_GCLAIM
-      __hip_atomic_store(&g_claim_ctr[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __threadfence();
-#endif
       // the mid units left their residues for segment s + grid: valid if it is
       // of the same range and every mid unit ran (p^2 < Vs for p <= TB)
       const uint32_t r0 = range_of(s), r1 = range_of(s + grid);
@@ -2083,7 +2020,7 @@ constexpr uint32_t kStageCap = 64;                 // keys per (wave, super-buck
 constexpr uint32_t kKeyShift = 20;                 // entry = LDS word index << 5 | bit < 2^20
 static_assert(IMG_WORDS * 32 <= (1u << kKeyShift) && kKeyShift + kSupLog <= 32, "bucket key layout");
 #ifndef DSE_BK_SORT_GROUP
-#define DSE_BK_SORT_GROUP 16
+#define DSE_BK_SORT_GROUP 64
 #endif
 constexpr uint32_t kSortGroup = DSE_BK_SORT_GROUP;  // band-1 workgroups per level-2 job
 #ifndef DSE_BK_SORT_TILE
