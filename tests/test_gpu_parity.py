@@ -328,6 +328,38 @@ def test_window_two_contexts_concurrently(ctx):
     assert got == want
 
 
+def _odd_primes_upto(n):
+    if n < 3:
+        return np.zeros(0, dtype=np.int64)
+    s = np.ones(n + 1, dtype=bool)
+    s[:2] = False
+    s[4::2] = False
+    for i in range(3, int(n ** 0.5) + 1, 2):
+        if s[i]:
+            s[i * i::2 * i] = False
+    p = np.nonzero(s)[0]
+    return p[p > 2]
+
+
+@pytest.mark.parametrize("limit", [3, 4, 9, 10, 97, 1_000, 316_227, 1_000_003, 1_048_577, 1_048_579, 2_097_153,
+                                   2_097_155, 2_457_601])
+def test_base_table_primes_exact(ctx, limit):
+    """The base table's p[] is every odd prime <= limit, in order, across the
+    one-workgroup build (limit <= 2,097,153: base_small_kernel, its 64 KiB
+    bitmap boundary at 1,048,577) and the multi-workgroup build above it."""
+    import torch
+    from mail_sieve_e import sieve as S
+    t = torch.zeros(S.base_table_bytes(limit), dtype=torch.uint8, device="cuda")
+    ctx.base_primes_dev_async(limit, t.data_ptr(), t.numel(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    hdr = t[:16].cpu().numpy()
+    count = int(hdr[:4].view(np.uint32)[0])
+    want = _odd_primes_upto(limit)
+    assert count == len(want) and int(hdr[8:16].view(np.uint64)[0]) == limit
+    P = t[16:16 + 4 * count].cpu().numpy().view(np.uint32)
+    assert np.array_equal(P.astype(np.int64), want)
+
+
 @pytest.mark.parametrize("limit", [316_227, 1_000_003, 5_000_011])
 def test_table_from_broadcast_primes(ctx, limit):
     """Ranks receive only the primes (dse_base_table_prime_bytes) and finish
