@@ -5,9 +5,7 @@
 // each one to the other machines (sieve.clj:139). Here the odd primes up to
 // sqrt(max value) are computed once, on the device, into a flat table
 // (dse_internal.h) that ranks can RCCL-broadcast as bytes:
-//   - limit <= kBaseSmallMax (2,097,153; N up to 4.4e12): base_small_kernel,
-//     one workgroup, sieve and ordered compaction in one launch;
-//   - up to kBaseLimitMax: base_mask_kernel (many workgroups, LDS slices)
+//   - limit <= kBaseLimitMax: base_mask_kernel (many workgroups, LDS slices)
 //     + an ordered count / scan / write compaction;
 //   - larger limits (high-offset windows, up to 2^31): the wheel kernel sieves
 //     [3, limit] from a first-level table, then the same compaction;
@@ -183,94 +181,6 @@ __global__ __launch_bounds__(kBaseMaskThreads) void base_mask_kernel(uint64_t li
   }
 }
 
-// Small tables in one workgroup (limit <= kBaseSmallMax: every chunk config
-// up to N = 4.4e12), one launch instead of four: the odd primes q <= 1,449
-// by trial division (a thread each), then thread t sieves its own run of the
-// odd values' bits in LDS (no atomics: a first multiple per prime by a float
-// quotient, then a plain OR per multiple), counts its primes, and after a
-// workgroup scan writes them to p[] in order. At N = 1e11 (limit 316,227)
-// it replaces base_mask_kernel and the three compaction kernels (~33 us of
-// kernel time, profiles/r06/rocprofv3_kernel_stats.csv).
-constexpr uint32_t kBaseSmallThreads = 1024;
-constexpr uint32_t kBaseSmallWords = 32768;                 // LDS bitmap: 128 KiB
-constexpr uint64_t kBaseSmallMax = 2ull * 32ull * kBaseSmallWords + 1;  // 2,097,153: odd values 3..limit fit
-constexpr uint32_t kBaseSmallQ = 256;                       // > pi(isqrt(kBaseSmallMax)) = 229
-static_assert(kBaseSmallWords % kBaseSmallThreads == 0, "whole words per thread");
-
-__global__ __launch_bounds__(kBaseSmallThreads) void base_small_kernel(uint64_t limit, void* __restrict__ table,
-                                                                       uint32_t cap) {
-  extern __shared__ uint32_t bm[];  // composite bits of the odd values 3 + 2g, g < nb (nw words)
-  __shared__ uint32_t s_q[kBaseSmallQ];
-  __shared__ uint32_t s_nq;
-  __shared__ uint32_t s_scan[kBaseSmallThreads];
-  const uint32_t tid = threadIdx.x;
-  const uint32_t nb = (uint32_t)((limit - 3) / 2 + 1);
-  const uint32_t nw = (nb + 31) / 32;
-  const uint32_t wpt = (nw + kBaseSmallThreads - 1) / kBaseSmallThreads;  // words per thread
-  const uint32_t w0 = tid * wpt, w1 = min(nw, w0 + wpt);
-  uint32_t r = (uint32_t)__builtin_sqrtf((float)limit);  // isqrt(limit), corrected below
-  while ((uint64_t)r * r > limit) --r;
-  while ((uint64_t)(r + 1) * (r + 1) <= limit) ++r;
-  if (tid == 0) s_nq = 0;
-  for (uint32_t w = w0; w < w1; ++w) bm[w] = 0;
-  __syncthreads();
-  // sieving primes: odd q <= isqrt(limit), one per thread by trial division
-  {
-    const uint32_t q = 3 + 2 * tid;
-    bool pr = q <= r;
-    for (uint32_t d = 3; pr && d * d <= q; d += 2) pr = q % d != 0;
-    if (pr) s_q[atomicAdd(&s_nq, 1u)] = q;
-  }
-  __syncthreads();
-  const uint32_t nq = s_nq;
-  // this thread's bits: odd indices [g0, g1)
-  const uint32_t g0 = 32 * w0, g1 = min(nb, 32 * w1);
-  for (uint32_t i = 0; i < nq && g0 < g1; ++i) {
-    const uint32_t q = s_q[i];
-    // first odd multiple v = q m >= max(q^2, 3 + 2 g0); index (v - 3) / 2, step q
-    const uint32_t vlo = max(q * q, 3 + 2 * g0);
-    uint32_t m = (uint32_t)((float)vlo / (float)q);  // within 1 of floor (vlo < 2^22)
-    while (m * q < vlo) ++m;
-    while (m > 1 && (m - 1) * q >= vlo) --m;
-    m |= 1u;  // odd multiples only (the next one if m is even)
-    for (uint32_t g = (q * m - 3) / 2; g < g1; g += q) bm[g >> 5] |= 1u << (g & 31);
-  }
-  // primes of this thread's run, then a workgroup scan for their slots
-  uint32_t c = 0;
-  for (uint32_t w = w0; w < w1; ++w) {
-    uint32_t v = ~bm[w];
-    if (32 * w + 32 > nb) v &= 32 * w >= nb ? 0u : (1u << (nb - 32 * w)) - 1;
-    c += __popc(v);
-  }
-  s_scan[tid] = c;
-  __syncthreads();
-  for (uint32_t o = 1; o < kBaseSmallThreads; o <<= 1) {
-    const uint32_t x = tid >= o ? s_scan[tid - o] : 0;
-    __syncthreads();
-    s_scan[tid] += x;
-    __syncthreads();
-  }
-  const uint32_t total = s_scan[kBaseSmallThreads - 1];
-  uint32_t* P = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(table) + 16);
-  uint32_t pos = s_scan[tid] - c;
-  for (uint32_t w = w0; w < w1; ++w) {
-    uint32_t v = ~bm[w];
-    if (32 * w + 32 > nb) v &= 32 * w >= nb ? 0u : (1u << (nb - 32 * w)) - 1;
-    while (v) {
-      const uint32_t b = __builtin_ctz(v);
-      v &= v - 1;
-      if (pos < cap) P[pos] = 3 + 2 * (32 * w + b);
-      ++pos;
-    }
-  }
-  if (tid == 0) {
-    TableHeader* h = reinterpret_cast<TableHeader*>(table);
-    h->count = total <= cap ? total : 0xFFFFFFFFu;
-    h->cap = cap;
-    h->limit = limit;
-  }
-}
-
 // out[j] = sum over i < nsrc of in[i * n + j] (the logical-device stand-in for
 // the count all-reduce, dse_debug_init_logical)
 __global__ __launch_bounds__(256) void sum_rows_kernel(const unsigned long long* __restrict__ in, uint32_t nsrc,
@@ -297,19 +207,6 @@ hipError_t launch_base_primes(uint64_t limit, void* table, uint32_t cap, hipStre
   if (limit < 3) {  // no odd primes: empty table
     TableHeader h{0, cap, limit};
     return hipMemcpyAsync(table, &h, sizeof(h), hipMemcpyHostToDevice, stream);
-  }
-  if (limit <= kBaseSmallMax) {
-    const uint32_t nw = (uint32_t)(((limit - 3) / 2 + 1 + 31) / 32);
-    const uint32_t lds = 4 * nw;
-    if (lds > 65536) {  // bitmaps above 64 KiB (limit > 1,048,577) need the attribute
-      const hipError_t ea = hipFuncSetAttribute(reinterpret_cast<const void*>(&base_small_kernel),
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, 4 * (int)kBaseSmallWords);
-      if (ea != hipSuccess) return ea;
-    }
-    hipLaunchKernelGGL(base_small_kernel, dim3(1), dim3(kBaseSmallThreads), lds, stream, limit, table, cap);
-    const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    return launch_wheel_offsets(table, 256, stream);  // m[] and a[]
   }
   // scratch carved from the table's m[]/a[] region (written last): [mask][block sums]
   char* mreg = reinterpret_cast<char*>(table) + table_m_offset(cap);

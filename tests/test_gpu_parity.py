@@ -344,9 +344,10 @@ def _odd_primes_upto(n):
 @pytest.mark.parametrize("limit", [3, 4, 9, 10, 97, 1_000, 316_227, 1_000_003, 1_048_577, 1_048_579, 2_097_153,
                                    2_097_155, 2_457_601])
 def test_base_table_primes_exact(ctx, limit):
-    """The base table's p[] is every odd prime <= limit, in order, across the
-    one-workgroup build (limit <= 2,097,153: base_small_kernel, its 64 KiB
-    bitmap boundary at 1,048,577) and the multi-workgroup build above it."""
+    """The base table's p[] is every odd prime <= limit, in order, from a
+    single odd value up to the largest one-level build (kBaseLimitMax =
+    2,457,601; round 6 measured a one-workgroup build of these tables, 79 us
+    against 34 us at 1e11, and dropped it)."""
     import torch
     from mail_sieve_e import sieve as S
     t = torch.zeros(S.base_table_bytes(limit), dtype=torch.uint8, device="cuda")

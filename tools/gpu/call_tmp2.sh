@@ -1,8 +1,10 @@
 set -o pipefail
-mkdir -p gpurun_out/c19
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_logical.py tests/test_gpu_rccl.py -m gpu -x -q -k "bucket or window or table" --timeout 300 --timeout-method thread > gpurun_out/c19/tests.log 2>&1 || { tail -30 gpurun_out/c19/tests.log; exit 1; }
-tail -2 gpurun_out/c19/tests.log
-for i in 1 2 3; do for v in prod head sg128 sg64t16k g1k2 g1k8; do if [ $v = prod ]; then unset DSE_LIB; else export DSE_LIB=variants/libdse_$v.so; fi; echo -n "$v: "; timeout -k 10 120 python tools/window_bench.py || exit 1; done; done
-unset DSE_LIB
-bash tools/gpu/window_kstats.sh head sg128 sg64t16k g1k2 g1k8 > gpurun_out/c19/kstats.txt 2>&1 || { tail -30 gpurun_out/c19/kstats.txt; exit 1; }
-grep "==\|window \[\|fill_stage\|bucket_sort" gpurun_out/c19/kstats.txt
+mkdir -p gpurun_out/c23
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/c23/tests.log 2>&1 || { tail -30 gpurun_out/c23/tests.log; exit 1; }
+tail -2 gpurun_out/c23/tests.log
+OUT=gpurun_out/c23 N=1e11 ROUNDS=4 TMO=700 bash tools/gpu/ab.sh head prod tb576 tb640 tb704 > /dev/null || exit 1
+OUT=gpurun_out/c23 N=1e12 ROUNDS=1 TMO=400 bash tools/gpu/ab.sh prod tb576 tb640 tb704 > /dev/null || exit 1
+cat gpurun_out/c23/ab_*.txt
+timeout -k 10 240 python tools/rank_steps.py 1e11 8 > gpurun_out/c23/rs_prod.txt 2>&1 || exit 1
+DSE_LIB=variants/libdse_head.so timeout -k 10 240 python tools/rank_steps.py 1e11 8 > gpurun_out/c23/rs_head.txt 2>&1 || exit 1
+grep -h "base table\|critical" gpurun_out/c23/rs_prod.txt gpurun_out/c23/rs_head.txt
