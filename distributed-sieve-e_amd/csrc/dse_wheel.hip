@@ -245,6 +245,9 @@ constexpr uint32_t kBlockMask = ~31u;  // period index -> its block's byte addre
 #endif
 // profiling knockout (DSE_FAKE_CF_L): the L marks' blocks forced to lane-distinct banks (wrong marks)
 constexpr uint32_t kBlockMaskL = DSE_FAKE_CF_L ? ~127u : kBlockMask;
+#ifndef DSE_FAKE_CF_INIT
+#define DSE_FAKE_CF_INIT 0
+#endif
 #ifndef DSE_SHORT_TAIL
 #define DSE_SHORT_TAIL 16
 #endif
@@ -1146,6 +1149,9 @@ __global__ __launch_bounds__(NT) void wheel_segments_kernel(const void* __restri
       const uint32_t o = (k0_o + x * kGInv30[g]) % Mg;                  // bit offset of period k0
       const uint32_t d0 = o >> 5, kc = d0 & 3;
       boff[g] = (kc * kGDW + gbase(g) + d0 - kc) / 4;                    // 16-byte block index
+#if DSE_FAKE_CF_INIT  // profiling knockout: a 16-lane read group on consecutive 16-byte blocks (wrong patterns)
+      boff[g] = gbase(g) / 4 + (lane & 15u);
+#endif
       bsh[g] = o & 31;
     }
     uint32_t* const wp = img + 8 * b0 + pl;
