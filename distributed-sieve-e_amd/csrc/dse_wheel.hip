@@ -95,7 +95,7 @@ static_assert(BLOCKS % (64 * NW) == 0, "expansion blocks");
 #endif
 constexpr uint32_t TA = DSE_TA;             // A/B1 threshold
 #ifndef DSE_TB1
-#define DSE_TB1 512
+#define DSE_TB1 640
 #endif
 constexpr uint32_t TB1 = DSE_TB1;           // B1/B2 threshold
 #ifndef DSE_TB
